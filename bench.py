@@ -1,0 +1,218 @@
+"""Headline benchmark: transcript MB/s scanned+redacted per node, and % of the HBM roofline.
+
+Workload (BASELINE.json configs[1], "config 2"): per GPU, 100k synthetic conversations x 100
+utterances = 10M utterances (~120 B, lognormal), one scan+redact pass with per-conversation
+expected_pii_type context.  A "step" = one pii_scan_redact_device call over the whole resident batch
+(+ the RCCL all-reduce of the per-infoType histogram, the only collective).  Inputs are resident in
+HBM before timing; outputs are written to HBM.  Multi-GPU: conversations are sharded by
+conversation id (each rank owns its own 100k conversations, weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+synth = importlib.import_module("context-based-pii_amd.synth")
+compiler = importlib.import_module("context-based-pii_amd.compiler")
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy ceiling
+METRIC = "transcript MB/s scanned+redacted per node (1/2/4/8 GPU) and % HBM roofline"
+
+# --------------------------------------------------------------------------- CPU baseline (oracle)
+_CPU = {}
+
+
+def _cpu_init(data, offs, role, conv, ts):
+    _CPU.update(data=data, offs=offs, role=role, conv=conv, ts=ts)
+
+
+def _cpu_work(rng):
+    from oracle import pii_oracle as O
+    cfg = O.RuleConfig.load()
+    d, o, r, c, t = _CPU["data"], _CPU["offs"], _CPU["role"], _CPU["conv"], _CPU["ts"]
+    lo, hi = rng
+    rows = [(int(c[i]), int(r[i]), d[int(o[i]):int(o[i + 1])].tobytes(), int(t[i])) for i in range(lo, hi)]
+    t0 = time.perf_counter()
+    O.process_rows(rows, cfg)
+    return time.perf_counter() - t0, int(o[hi] - o[lo])
+
+
+def cpu_baseline(bank, seconds: float = 15.0):
+    """The oracle (Python re + validators), multi-process over whole conversations on the host."""
+    cores = min(16, os.cpu_count() or 1)
+    meta = synth.corpus_meta(4000, 100, bank, seed=synth.SEED + 7)
+    data = synth.gather_bytes(meta, bank)
+    offs = meta.offsets.astype(np.int64)
+    # calibrate on one conversation block, then size the sample to ~`seconds` of wall time
+    _cpu_init(data, offs, meta.role, meta.conv_slot, meta.ts_us)
+    dt, nb = _cpu_work((0, 1000))
+    rate1 = nb / max(dt, 1e-6)
+    target_bytes = rate1 * cores * seconds
+    n_conv = int(min(4000, max(cores, target_bytes / (nb / 10))))
+    chunks = [(i * 100, (i + 1) * 100) for i in range(n_conv)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores, initializer=_cpu_init, initargs=(data, offs, meta.role, meta.conv_slot, meta.ts_us)) as pool:
+        res = pool.map(_cpu_work, chunks, chunksize=max(1, len(chunks) // (cores * 4)))
+    wall = time.perf_counter() - t0
+    nbytes = sum(b for _, b in res)
+    return {"value": round(nbytes / wall / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
+            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e6:.1f} MB) of the same synthetic "
+                      f"distribution, oracle/pii_oracle.py process_rows, multiprocessing fork pool, wall {wall:.1f}s"}
+
+
+# --------------------------------------------------------------------------- GPU corpus assembly
+def gpu_corpus(meta, bank, dev):
+    import torch
+    bank_data = torch.from_numpy(bank.data).to(dev)
+    bank_off = torch.from_numpy(bank.offsets).to(dev)
+    bid = torch.from_numpy(meta.bank_id.astype(np.int64)).to(dev)
+    offs = torch.from_numpy(meta.offsets.view(np.int64)).to(dev)
+    total = int(meta.offsets[-1])
+    text = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    n = meta.n
+    step = 1 << 20
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        b = bid[lo:hi]
+        lens = bank_off[b + 1] - bank_off[b]
+        o0 = offs[lo:hi]
+        nb = int(offs[hi] - offs[lo])
+        rep = torch.repeat_interleave(bank_off[b] - o0, lens)
+        idx = torch.arange(int(offs[lo]), int(offs[lo]) + nb, device=dev, dtype=torch.int64) + rep
+        text[int(offs[lo]):int(offs[lo]) + nb] = bank_data[idx]
+    return text, offs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--conversations", type=int, default=100_000, help="per GPU")
+    ap.add_argument("--utt-per-conv", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    bank = synth.build_bank(16384, 16384, seed=synth.SEED)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(bank, args.cpu_seconds)          # before any HIP initialisation (fork pool)
+
+    import torch
+    import torch.distributed as dist
+    eng_mod = importlib.import_module("context-based-pii_amd.engine")
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # this rank's shard: conversations [rank*C, (rank+1)*C) -- the conversation-id sharding of
+    # SURVEY §8(e) (gpu = conversation_id % G on a dense id space)
+    C, U = args.conversations, args.utt_per_conv
+    meta = synth.corpus_meta(C, U, bank, seed=synth.SEED, conv_base=rank * C)
+    text, offs = gpu_corpus(meta, bank, dev)
+    n = meta.n
+    n_bytes = int(meta.offsets[-1])
+    slot = torch.from_numpy((meta.conv_slot - rank * C).view(np.int32)).to(dev)
+    role = torch.from_numpy(meta.role).to(dev)
+    ts = torch.from_numpy(meta.ts_us).to(dev)
+    out_cap = n_bytes + 48 * n
+    span_cap = n * 2
+    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
+    d_ctx = torch.empty(n, dtype=torch.int16, device=dev)
+    comp = compiler.compile_default()
+    eng = eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
+    T = len(eng.type_names)
+    hist = torch.zeros(T + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        eng.scan_redact_device(text.data_ptr(), offs.data_ptr(), n, slot.data_ptr(), role.data_ptr(),
+                               ts.data_ptr(), d_out.data_ptr(), out_cap, d_oo.data_ptr(), d_sp.data_ptr(),
+                               span_cap, d_ctx.data_ptr())
+        ob, ns, fl = eng.sync()
+        if fl:
+            raise RuntimeError(f"engine error flags {fl}")
+        if world > 1:
+            h = torch.from_numpy(eng.histogram().astype(np.int64)).to(dev)
+            hist[:T] = h
+            hist[T] = ns
+            dist.all_reduce(hist)                           # RCCL over xGMI: per-infoType counts
+        return ob, ns
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    per_kernel = np.zeros(6)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ob, ns = step()
+        per_kernel += np.array(eng.timings())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    per_kernel /= args.steps
+    ms_step = elapsed / args.steps * 1e3
+    total_bytes = n_bytes * world * args.steps
+    mbps = total_bytes / elapsed / 1e6
+    # algorithmic bytes: in + out + in/out offsets + slot/role + spans
+    B = n_bytes + ob + 8 * (n + 1) * 2 + 5 * n + 16 * ns
+    t_pipe = per_kernel[5] / 1e3
+    # dominant kernel: the reverse DFA scan; algorithmic bytes per launch = utterance bytes read +
+    # 8(U+1) offsets + U roles + U*(4+2) per-row event count / context results written
+    scan_B = n_bytes + 8 * (n + 1) + n + 6 * n
+    t_scan = per_kernel[0] / 1e3
+    scan_GBps = scan_B / t_scan / 1e9
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "config2: per GPU 100k conversations x 100 utterances (10M utterances, "
+                                   "~120 B lognormal) single-utterance scan+redact with expected_pii_type context",
+                       "utterances_per_gpu": n, "bytes_per_gpu": n_bytes, "parallelism": f"conversation-sharded x{world}",
+                       "rules": "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
+            "utt_per_s": round(n * world * args.steps / elapsed, 1),
+            "spans_per_step_per_gpu": ns,
+            "kernels_ms": {k: round(float(v), 4) for k, v in zip(
+                ["scan", "context", "resolve", "offsets", "redact", "pipeline"], per_kernel)},
+            "pipeline": {"algorithmic_bytes": int(B), "GBps": round(B / t_pipe / 1e9, 1),
+                         "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
+            "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": None},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

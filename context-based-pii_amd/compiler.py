@@ -856,7 +856,6 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     if scan_d.n_classes + 1 > 255 or scan_k.n_classes + 1 > 255:
         raise RuleError("too many byte classes")
     cmap2 = scan_d.cmap.astype(np.uint16) | (scan_k.cmap.astype(np.uint16) << 8)
-    d_off, d_ids = _acc_tables(scan_d)
     k_off, k_ids = _acc_tables(scan_k)
 
     # ---- FIRST: one anchored leftmost-first DFA per detector pattern ----
@@ -920,6 +919,23 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
             rule_off[v * T + t + 1] = len(rule_ids)
             excl_ids.extend(per_type_excl[t])
             excl_off[v * T + t + 1] = len(excl_ids)
+    # excluder patterns (their type is excluded-against in some variant) get a slot in the resolve
+    # kernel's private state and come FIRST in every SCAN-D accept set, so that a same-start
+    # excluder is known before the findings it may exclude (A.5).
+    excluder_types = set(excl_ids[:int(excl_off[-1])])
+    excluded_types = {t for v in range(V) for t in range(T) if excl_off[v * T + t + 1] > excl_off[v * T + t]}
+    if excluder_types & excluded_types:
+        raise RuleError("an infoType that is both excluded and excluding is not supported")
+    exidx = np.full(P, 0xFF, dtype=np.uint8)
+    ne = 0
+    for p in rules.patterns:
+        if rules.type_id[p.type_name] in excluder_types:
+            exidx[p.pid] = ne
+            ne += 1
+    if ne > 8:
+        raise RuleError("more than 8 excluder patterns")
+    scan_d.acc_sets = [tuple(sorted(s, key=lambda pid: (exidx[pid] == 0xFF, pid))) for s in scan_d.acc_sets]
+    d_off, d_ids = _acc_tables(scan_d)
     hot = []
     for hr in hot_rules:
         n3 = NFA()
@@ -971,6 +987,7 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     S["det.type"] = np.array([rules.type_id[p.type_name] for p in rules.patterns], dtype=np.uint16)
     S["det.validator"] = np.array([VALIDATOR_IDS[p.validator] for p in rules.patterns], dtype=np.uint8)
     S["det.lik"] = np.array([p.likelihood for p in rules.patterns], dtype=np.uint8)
+    S["det.exidx"] = exidx
     S["det.first_desc"] = first_desc.reshape(-1)
     S["hot.rule"] = hot_desc.reshape(-1)
     S["hot.dfa_desc"] = hot_dfa_desc.reshape(-1)

@@ -257,9 +257,22 @@ class Corpus:
         return len(self.role)
 
 
-def make_corpus(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, conv_base: int = 0) -> Corpus:
+@dataclass
+class CorpusMeta:
+    bank_id: np.ndarray     # int32 [n]
+    offsets: np.ndarray     # uint64 [n+1]
+    conv_slot: np.ndarray   # uint32 [n]
+    role: np.ndarray        # uint8 [n]
+    ts_us: np.ndarray       # int64 [n]
+
+    @property
+    def n(self):
+        return len(self.role)
+
+
+def corpus_meta(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, conv_base: int = 0) -> CorpusMeta:
     """Conversation-major layout: conversation c's rows are contiguous and in entry order,
-    alternating AGENT / END_USER, 5 s apart (the pinned batch contract, include/pii_engine.h)."""
+    alternating AGENT / END_USER, 5 s apart (the batch contract of include/pii_engine.h)."""
     g = np.random.Generator(np.random.PCG64(seed + conv_base))
     n = n_conv * utt_per_conv
     n_agent = int((bank.roles == ROLE_AGENT).sum())
@@ -271,12 +284,23 @@ def make_corpus(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, co
     lens = (bank.offsets[1:] - bank.offsets[:-1])[bid]
     offs = np.zeros(n + 1, dtype=np.uint64)
     np.cumsum(lens, out=offs[1:])
-    # gather bytes: for each output byte, source index = bank_off[bid] + (k - out_off)
-    total = int(offs[-1])
-    src_start = bank.offsets[:-1][bid].astype(np.int64)
-    rep = np.repeat(src_start - offs[:-1].astype(np.int64), lens)
-    idx = np.arange(total, dtype=np.int64) + rep
-    data = bank.data[idx]
     conv = (np.repeat(np.arange(n_conv, dtype=np.uint32), utt_per_conv) + np.uint32(conv_base)).astype(np.uint32)
     ts = (1_760_000_000_000_000 + pos.astype(np.int64) * 5_000_000).astype(np.int64)
-    return Corpus(data, offs, conv, role, ts, bid)
+    return CorpusMeta(bid, offs, conv, role, ts)
+
+
+def gather_bytes(meta: CorpusMeta, bank: Bank, lo: int = 0, hi: int = None) -> np.ndarray:
+    """Bytes of rows [lo, hi) (numpy; use for small corpora or samples)."""
+    hi = meta.n if hi is None else hi
+    bid = meta.bank_id[lo:hi]
+    lens = (bank.offsets[1:] - bank.offsets[:-1])[bid]
+    total = int(lens.sum())
+    out_off = np.zeros(len(bid) + 1, dtype=np.int64)
+    np.cumsum(lens, out=out_off[1:])
+    rep = np.repeat(bank.offsets[:-1][bid].astype(np.int64) - out_off[:-1], lens)
+    return bank.data[np.arange(total, dtype=np.int64) + rep]
+
+
+def make_corpus(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, conv_base: int = 0) -> Corpus:
+    m = corpus_meta(n_conv, utt_per_conv, bank, seed, conv_base)
+    return Corpus(gather_bytes(m, bank), m.offsets, m.conv_slot, m.role, m.ts_us, m.bank_id)

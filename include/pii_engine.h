@@ -1,0 +1,127 @@
+/*
+ * pii_engine.h - C ABI of the MI355X PII scan-and-redact engine (libpii.so).
+ *
+ * Drop-in boundary for the de-identification step of iyngr/context-based-pii:
+ *
+ *   main_service/main.py:580  call_dlp_for_redaction(transcript, context) -> str
+ *       builds a DLP request (main.py:596-726) and calls
+ *   main_service/main.py:728  dlp_client.deidentify_content(request=...)
+ *
+ * The engine replaces the remote DLP call AND the Redis context record the handlers keep
+ * (main.py:366-374 SETEX context:{conversation_id}, TTL CONTEXT_TTL_SECONDS=90, main.py:163;
+ * GET at main.py:403/444): per-conversation context lives in HBM, indexed by a caller-chosen
+ * conversation SLOT (the Python shim maps conversation_id strings to slots).
+ *
+ * One engine per GPU; calls on one engine are serialised by the caller (not re-entrant), exactly
+ * like one gunicorn worker's DLP client (main_service/Dockerfile:29).  Plain pointers and sizes only.
+ *
+ * Batch contract (pii_scan_redact*): rows are utterances in arrival order.  Rows of one
+ * conversation must be contiguous in the batch and in original_entry_index order (the replay /
+ * ingest order); a slot that appears in two separate runs of one batch is rejected with
+ * PII_E_ORDER.  AGENT rows are redacted without context and then update their conversation's
+ * context from the context keywords (handle_agent_utterance, main.py:344-384); CUSTOMER rows are
+ * redacted with the conversation's live context (handle_customer_utterance, main.py:386-425);
+ * OTHER rows are redacted without context and leave it unchanged.
+ */
+#ifndef PII_ENGINE_H
+#define PII_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes; the Python shim maps them onto the reference's error strings
+ * ([DLP_PROCESSING_ERROR] {transcript} ..., main.py:752-773) */
+#define PII_OK 0
+#define PII_E_ARG -1       /* bad argument / malformed offsets                              */
+#define PII_E_RULES -2     /* rules blob malformed or unsupported                           */
+#define PII_E_DEVICE -3    /* HIP runtime error                                             */
+#define PII_E_CAPACITY -4  /* out_cap or span_cap too small: required sizes written back    */
+#define PII_E_ORDER -5     /* a conversation slot appears in two runs of one batch          */
+#define PII_E_NOMEM -6     /* device allocation failed                                      */
+
+#define PII_ROLE_CUSTOMER 0 /* END_USER / CUSTOMER (subscriber_service/main.py:229) */
+#define PII_ROLE_AGENT 1    /* AGENT (subscriber_service/main.py:200)              */
+#define PII_ROLE_OTHER 2
+
+/* one kept finding: byte offsets into the UTF-8 input of row `utt` */
+typedef struct pii_span {
+    uint32_t utt;
+    uint32_t start;
+    uint32_t end;
+    uint16_t info_type;  /* index into the engine's type table (pii_type_name) */
+    uint8_t likelihood;  /* DLP scale: 1 VERY_UNLIKELY .. 5 VERY_LIKELY         */
+    uint8_t flags;
+} pii_span;
+
+typedef struct pii_info {
+    uint32_t n_types;          /* info types (YAML info_types, custom types, build-defined)  */
+    uint32_t n_patterns;       /* detector patterns                                          */
+    uint32_t n_context_groups; /* context_keywords groups (dlp_config.yaml:5-91)              */
+    uint32_t n_conv_slots;
+    uint32_t scan_states_d;    /* SCAN prefilter automaton states                             */
+    uint32_t scan_states_k;    /* context-keyword automaton states                            */
+    uint32_t scan_lds_bytes;   /* LDS the scan kernel needs per workgroup                     */
+    uint32_t reserved;
+} pii_info;
+
+/* Rules blob = output of context-based-pii_amd/compiler.py (compiled dlp_config.yaml).
+ * Replaces: the DLP inspect/deidentify templates (deployment/update_dlp_templates.py:38-78). */
+int pii_engine_create(const void* rules_blob, size_t blob_bytes, int device, uint32_t n_conv_slots,
+                      int64_t context_ttl_us, struct pii_engine** out);
+int pii_engine_destroy(struct pii_engine* e);
+int pii_engine_info(struct pii_engine* e, pii_info* out);
+/* name of info type `t` ("CREDIT_CARD_NUMBER"); returns its length or a negative error */
+int pii_type_name(struct pii_engine* e, uint32_t t, char* buf, size_t cap);
+/* name of the context group `g` (its expected_pii_type) */
+int pii_context_group_type(struct pii_engine* e, uint32_t g);
+const char* pii_last_error(struct pii_engine* e);
+
+/* Host-buffer entry point (replaces call_dlp_for_redaction for a batch of transcripts).
+ *   bytes/offsets : n_utt rows, row i = bytes[offsets[i] .. offsets[i+1])
+ *   conv_slot     : conversation slot per row (< n_conv_slots)
+ *   role          : PII_ROLE_* per row
+ *   ts_us         : per-row timestamp (start_timestamp_usec) for the context TTL; NULL = no expiry
+ *   out_bytes     : redacted rows, packed; out_offsets[n_utt+1]
+ *   spans         : kept findings ordered by (utt, start); *n_spans = count
+ *   ctx_info      : optional int16[n_utt]: AGENT rows -> context group stored (-1 none),
+ *                   CUSTOMER rows -> context group used (-1 none), OTHER -> -1
+ * On PII_E_CAPACITY, out_offsets[n_utt] = required bytes and *n_spans = required spans, and the
+ * conversation context is NOT updated (the call can be retried). */
+int pii_scan_redact(struct pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                    const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us,
+                    uint8_t* out_bytes, uint64_t out_cap, uint64_t* out_offsets,
+                    pii_span* spans, uint32_t span_cap, uint32_t* n_spans, int16_t* ctx_info);
+
+/* Device-buffer entry point: every pointer is device memory (inputs already resident in HBM).
+ * Work is enqueued on `stream` (NULL = the engine's stream) and returns without waiting; call
+ * pii_sync() for the totals.  d_bytes is read in aligned 16-byte chunks that stay inside
+ * [d_bytes, d_bytes + offsets[n_utt]). */
+int pii_scan_redact_device(struct pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                           uint32_t n_utt, const uint32_t* d_conv_slot, const uint8_t* d_role,
+                           const int64_t* d_ts_us, uint8_t* d_out_bytes, uint64_t out_cap,
+                           uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
+                           int16_t* d_ctx_info, void* stream);
+/* wait for the last device call; totals[0] = output bytes, [1] = spans, [2] = error flags */
+int pii_sync(struct pii_engine* e, uint64_t totals[3]);
+
+/* per-conversation context record (replaces redis GET/SETEX of context:{id}) */
+int pii_context_get(struct pii_engine* e, uint32_t slot, int32_t* group, int64_t* ts_us);
+int pii_context_set(struct pii_engine* e, uint32_t slot, int32_t group, int64_t ts_us);
+
+/* per-info-type counts of kept findings since the last reset (counts[n_types]); the multi-GPU
+ * driver all-reduces these over RCCL */
+int pii_histogram(struct pii_engine* e, uint64_t* counts, uint32_t n);
+int pii_histogram_reset(struct pii_engine* e);
+
+/* per-kernel device time of the last call, milliseconds (HIP events on the engine stream):
+ * [0] scan [1] context [2] resolve [3] offsets [4] redact [5] total */
+int pii_last_timings(struct pii_engine* e, float ms[6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PII_ENGINE_H */
