@@ -35,41 +35,44 @@ __device__ inline bool v_luhn(const uint8_t* q, int n) {
     return cnt >= 2 && s % 10 == 0;
 }
 
-// first up-to-`cap` digits of q; returns the digit count
-__device__ inline int collect_digits(const uint8_t* q, int n, uint8_t* d, int cap) {
-    int k = 0;
-    for (int i = 0; i < n; ++i) {
-        uint32_t c = q[i];
-        if (is_digit(c)) {
-            if (k < cap) d[k] = (uint8_t)c;
-            ++k;
-        }
-    }
-    return k;
-}
-
+// digit-field validators accumulate the fields on the fly (no local arrays -> no scratch)
 __device__ inline bool v_nanp(const uint8_t* q, int n) {
-    uint8_t d[10];
-    int k = collect_digits(q, n, d, 10);
-    return k == 10 && d[0] >= '2' && d[3] >= '2';
+    int k = 0;
+    bool ok = true;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t c = q[i];
+        if (!is_digit(c)) continue;
+        if ((k == 0 || k == 3) && c < '2') ok = false;
+        ++k;
+    }
+    return ok && k == 10;
 }
 
 __device__ inline bool v_ssn(const uint8_t* q, int n) {
-    uint8_t d[9];
-    int k = collect_digits(q, n, d, 9);
-    if (k != 9) return false;
-    bool a000 = d[0] == '0' && d[1] == '0' && d[2] == '0';
-    bool a666 = d[0] == '6' && d[1] == '6' && d[2] == '6';
-    bool g00 = d[3] == '0' && d[4] == '0';
-    bool s0 = d[5] == '0' && d[6] == '0' && d[7] == '0' && d[8] == '0';
-    return !a000 && !a666 && d[0] != '9' && !g00 && !s0;
+    int k = 0;
+    uint32_t area = 0, group = 0, serial = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t c = q[i];
+        if (!is_digit(c)) continue;
+        const uint32_t d = c - '0';
+        if (k < 3) area = area * 10 + d;
+        else if (k < 5) group = group * 10 + d;
+        else serial = serial * 10 + d;
+        ++k;
+    }
+    return k == 9 && area != 0 && area != 666 && area < 900 && group != 0 && serial != 0;
 }
 
 __device__ inline bool v_ein(const uint8_t* q, int n) {
-    uint8_t d[9];
-    int k = collect_digits(q, n, d, 9);
+    int k = 0;
+    uint32_t p = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t c = q[i];
+        if (!is_digit(c)) continue;
+        if (k < 2) p = p * 10 + (c - '0');
+        ++k;
+    }
     if (k != 9) return false;
-    uint32_t p = (d[0] - '0') * 10u + (d[1] - '0');
     const uint64_t lo = 0xfffdffffcff1fc7eull, hi = 0x0000000cfdff3f9full;   // oracle EIN_PREFIXES
     return p < 64 ? ((lo >> p) & 1) : ((hi >> (p - 64)) & 1);
 }
@@ -94,12 +97,14 @@ __device__ inline bool v_ipv4(const uint8_t* q, int n) {
     return parts == 4;
 }
 
-__device__ inline bool v_swift(const uint8_t* q, int n) {
-    // ISO 3166-1 alpha-2, bit (a-'A')*26 + (b-'A')  (oracle ISO3166)
-    const uint32_t iso[22] = {0xeedf5978u, 0xdeddbdefu, 0x15843f27u, 0x0e00d480u, 0xb0095c00u, 0x0015fb9fu,
+// ISO 3166-1 alpha-2, bit (a-'A')*26 + (b-'A')  (oracle ISO3166)
+__constant__ const uint32_t ISO3166_BITS[22] = {0xeedf5978u, 0xdeddbdefu, 0x15843f27u, 0x0e00d480u, 0xb0095c00u, 0x0015fb9fu,
                               0x7818068du, 0x0340400fu, 0xf42b1d00u, 0xfd4f8141u, 0x25d7fffcu, 0x0100084bu,
                               0x538f3c40u, 0x40000001u, 0xfdf15100u, 0x9fbb3ae7u, 0x0410419au, 0x00408557u,
                               0x00004002u, 0x00100000u, 0x00400408u, 0x00000001u};
+
+__device__ inline bool v_swift(const uint8_t* q, int n) {
+    const uint32_t* iso = ISO3166_BITS;
     if (n != 8 && n != 11) return false;
     uint32_t a = q[4] - 'A', b = q[5] - 'A';
     if (a >= 26u || b >= 26u) return false;
@@ -151,21 +156,56 @@ struct Pool {
     const uint8_t* cmap;
 };
 
+template <int K>
+__device__ __forceinline__ uint32_t chunk_byte(const uint4& w) {
+    const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
+    return (x >> ((K & 3) * 8)) & 0xffu;
+}
+
+// Text access for the DFA runners: aligned 16-byte chunks (one chunk prefetched ahead) with
+// compile-time byte extraction, instead of one dependent byte load per DFA step.  A chunk is only
+// loaded when it contains at least one byte of the requested range; an aligned 16-byte block never
+// straddles a page, so reading all of it is safe.
+#define PII_DFA_STREAM(BODY)                                                                      \
+    {                                                                                             \
+        const uint8_t* pa = text + lo;                                                            \
+        const uint4* cp = reinterpret_cast<const uint4*>((uintptr_t)pa & ~(uintptr_t)15);         \
+        int j = lo - (int)((uintptr_t)pa & 15);   /* position of byte 0 of chunk *cp */           \
+        uint4 w = *cp;                                                                            \
+        uint4 wn = j + 16 < hi ? cp[1] : w;                                                       \
+        for (;;) {                                                                                \
+            const uint4 cur = w;                                                                  \
+            w = wn;                                                                               \
+            if (j + 32 < hi) wn = cp[2];                                                          \
+            BODY(0) BODY(1) BODY(2) BODY(3) BODY(4) BODY(5) BODY(6) BODY(7)                       \
+            BODY(8) BODY(9) BODY(10) BODY(11) BODY(12) BODY(13) BODY(14) BODY(15)                 \
+            j += 16;                                                                              \
+            ++cp;                                                                                 \
+            if (j >= hi) break;                                                                   \
+        }                                                                                         \
+    }
+
 // Anchored leftmost-first run of FIRST DFA `d` from byte s of text[0, L): returns the end `re`
 // would report for a match starting at s, or -1.  (compiler.build_first_dfa: flags bit0 = a match
 // ended before the char just consumed, bit1 = terminal.)
-__device__ inline int first_run(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L) {
+__device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L) {
     const uint16_t* tr = pool.trans + d[0];
     const uint8_t* fl = pool.flags + d[1];
     const uint8_t* cm = pool.cmap + d[2];
     const int nc = d[3];
     int st = s == 0 ? d[4] : (is_word(text[s - 1]) ? d[5] : d[6]);
     int last = -1;
-    for (int j = s; j < L; ++j) {
-        st = tr[st * nc + cm[text[j]]];
-        uint32_t f = fl[st];
-        if (f & 1) last = j;
-        if (f & 2) return last;
+    if (s < L) {
+        const int lo = s, hi = L;
+#define PII_FIRST_STEP(K)                                                                         \
+        if (j + (K) >= lo && j + (K) < hi) {                                                      \
+            st = tr[st * nc + cm[chunk_byte<K>(cur)]];                                            \
+            const uint32_t f = fl[st];                                                            \
+            if (f & 1) last = j + (K);                                                            \
+            if (f & 2) return last;                                                               \
+        }
+        PII_DFA_STREAM(PII_FIRST_STEP)
+#undef PII_FIRST_STEP
     }
     st = tr[st * nc + nc - 1];
     if (fl[st] & 1) last = L;
@@ -173,15 +213,20 @@ __device__ inline int first_run(const Pool& pool, const int32_t* d, const uint8_
 }
 
 // Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics)
-__device__ inline bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
+__device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
     const uint16_t* tr = pool.trans + d[0];
     const uint8_t* fl = pool.flags + d[1];
     const uint8_t* cm = pool.cmap + d[2];
     const int nc = d[3];
     int st = d[4];
-    for (int j = lo; j < hi; ++j) {
-        st = tr[st * nc + cm[text[j]]];
-        if (fl[st]) return true;
+    if (lo < hi) {
+#define PII_HOT_STEP(K)                                                                           \
+        if (j + (K) >= lo && j + (K) < hi) {                                                      \
+            st = tr[st * nc + cm[chunk_byte<K>(cur)]];                                            \
+            if (fl[st]) return true;                                                              \
+        }
+        PII_DFA_STREAM(PII_HOT_STEP)
+#undef PII_HOT_STEP
     }
     st = tr[st * nc + nc - 1];
     return fl[st] != 0;

@@ -5,13 +5,17 @@
 //   main.py:580-773), and the Redis context record main.py:366-374 / 403.
 //
 // Pipeline per batch (one HIP stream, no host round trip until pii_sync):
-//   k_chunk_index  lane -> utterance ranges of ~BYTES_PER_LANE bytes (load balance, no halo needed)
+//   k_chunk_index  lane -> utterance ranges of ~BYTES_PER_LANE bytes (load balance, no halo needed);
+//                  per-row defaults
+//   k_bounds       utterance-start bitmap aligned with the scan's 64-byte blocks
 //   k_scan         REVERSE two-automaton DFA scan, tables in LDS.  D = relaxed detector prefilter,
-//                  K = exact context keywords.  Emits candidate STARTS (events) per utterance and the
-//                  agent-row context group (extract_expected_pii, main.py:558-578)
+//                  K = exact context keywords.  Emits candidate STARTS (events) per lane
+//   k_pairs        agent-row context group (extract_expected_pii, main.py:558-578); (start, pattern)
+//                  pair queue
 //   k_ctx_scan / k_ctx_apply   per-conversation context (Redis SETEX/GET + TTL) as a segmented scan
-//   k_resolve      per utterance: leftmost-first confirmation (FIRST DFAs), validators, hotword
-//                  windows (HOT DFAs), exclusion, overlap resolution, output sizing
+//   k_pair_first   leftmost-first confirmation of every pair (FIRST DFAs in LDS)
+//   k_pair_eval    validators + hotword windows (HOT DFAs in LDS) under the row's context variant
+//   k_select       finditer skipping, exclusion, overlap resolution, output sizing
 //   k_scan_*       exclusive scans -> output byte offsets and span offsets
 //   k_finalize     capacity / error check (device side)
 //   k_redact       prefix-sum scatter of kept bytes and "[INFO_TYPE]" tokens, span list, histogram
@@ -31,20 +35,21 @@ using namespace pii;
 
 namespace {
 
-constexpr int P_MAX = 64;          // detector patterns handled by k_resolve's private state
-constexpr int NE_MAX = 8;          // excluder patterns
+constexpr int P_MAX = 64;          // detector patterns handled by k_select's private state
+constexpr int NE_MAX = 4;          // excluder patterns
 constexpr int SCAN_BLOCK = 512;
 constexpr int CTX_BLOCK = 1024;
 constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
-constexpr uint32_t BYTES_PER_LANE = 2048;
+constexpr uint32_t BYTES_PER_LANE = 512;
 constexpr int KW_NONE = 0x7fff;
 
-enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4 };
+enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8 };
 
 struct Event {
     uint32_t pos;   // candidate start, relative to the utterance
-    uint32_t acc;   // SCAN-D accept-set id of the transition that reported it
+    uint16_t sd;    // D automaton row (state * CD) BEFORE the reporting transition
+    uint16_t sk;    // K automaton row before it
 };
 
 struct RulesDev {
@@ -77,8 +82,13 @@ struct RulesDev {
 };
 
 // ------------------------------------------------------------------------------- k_chunk_index
-__global__ void k_chunk_index(const uint64_t* __restrict__ offs, uint32_t n_utt, uint32_t n_chunks,
-                              uint32_t* __restrict__ first_utt) {
+// first_utt[c] = first utterance starting at or after byte c*BYTES_PER_LANE (c in [0, n_chunks]);
+// also writes every row's defaults (no findings: out_len = len, n_find = 0; keyword group = the
+// always-present group for AGENT rows, else -1) with coalesced stores.
+__global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role, uint32_t n_utt,
+                              uint32_t n_chunks, int kw_always, uint32_t* __restrict__ first_utt,
+                              uint32_t* __restrict__ out_len, uint32_t* __restrict__ n_find,
+                              int16_t* __restrict__ kw) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u > n_utt) return;
     const uint64_t base = offs[0];
@@ -88,54 +98,130 @@ __global__ void k_chunk_index(const uint64_t* __restrict__ offs, uint32_t n_utt,
     uint64_t c_hi = (u == n_utt) ? n_chunks : su / BYTES_PER_LANE;
     if (c_hi > n_chunks) c_hi = n_chunks;
     for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
+    if (u < n_utt) {
+        out_len[u] = (uint32_t)(offs[u + 1] - offs[u]);
+        n_find[u] = 0;
+        kw[u] = (int16_t)((role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1);
+    }
 }
 
 // ------------------------------------------------------------------------------------- k_scan
-__device__ __forceinline__ uint32_t byte_of(const uint4& w, int k) {
-    uint32_t x = (k & 8) ? ((k & 4) ? w.w : w.z) : ((k & 4) ? w.y : w.x);
-    return (x >> ((k & 3) * 8)) & 0xffu;
-}
-
+// Each lane owns the utterances whose START falls in its BYTES_PER_LANE slice of the batch, i.e. one
+// contiguous byte range, and walks it right to left in aligned 64-byte blocks (the next block is
+// prefetched while the current one is stepped).  Per 16 bytes the byte-class lookups are issued first
+// (independent of the automaton state), then the two automata take 16 dependent steps.  Utterance
+// boundaries are crossed in-stream: reaching an utterance's first byte applies the end-of-text pseudo
+// class (the "start of text" of the reverse automata) and resets the state.  A transition with bit 15
+// set appends {pos, previous D row, previous K row} to the lane's event region; nothing is written
+// per utterance (k_chunk_index wrote the defaults).
 template <int K>
 __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
     const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
     return (x >> ((K & 3) * 8)) & 0xffu;
 }
 
-struct ScanLane {
-    uint32_t sd, sk, cnt, kmask;
-    int kwmin;
-    Event* evu;
-    int64_t s;
-};
-
-__device__ __forceinline__ void scan_step(const RulesDev& R, const uint16_t* s_cmap, const uint16_t* s_td,
-                                          const uint16_t* s_tk, ScanLane& L, uint32_t b, int64_t j) {
-    const uint32_t cc = s_cmap[b];
-    const uint32_t nd = s_td[L.sd + (cc & 0xffu)];
-    const uint32_t nk = s_tk[L.sk + (cc >> 8)];
-    if (__builtin_expect(((nd | (nk & L.kmask)) & 0x8000u) != 0, 0)) {
-        if (nd & 0x8000u) {
-            Event e;
-            e.pos = (uint32_t)(j + 1 - L.s);
-            e.acc = R.d_accid[L.sd + (cc & 0xffu)];
-            L.evu[L.cnt++] = e;
+// Utterance-start bitmap: bit k of word w <=> a non-empty utterance starts at text position
+// 64*w - mis + k - (word 0 offset), where mis = (text address) & 63, i.e. the bitmap words line up with
+// the scan's aligned 64-byte blocks.  The owner of a word (the first utterance starting in it) writes
+// it and zero-fills the words up to the next owner, so every word is written exactly once.
+__global__ void k_bounds(const uint64_t* __restrict__ offs, uint32_t n_utt, int64_t mis,
+                         uint64_t* __restrict__ bnd) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n_utt) return;
+    const int64_t w0 = ((int64_t)offs[0] + mis) >> 6;
+    const int64_t wu = ((int64_t)offs[u] + mis) >> 6;
+    if (u > 0 && (((int64_t)offs[u - 1] + mis) >> 6) == wu) return;      // not the owner
+    uint64_t bits = 0;
+    uint32_t v = u;
+    int64_t wn;
+    for (;; ++v) {
+        if (v == n_utt) {
+            wn = ((int64_t)offs[n_utt] - 1 + mis) >> 6;
+            wn = wn < wu ? wu + 1 : wn + 1;
+            break;
         }
-        if (nk & L.kmask & 0x8000u) {
-            const int g = R.k_acc_min[R.k_accid[L.sk + (cc >> 8)]];
-            L.kwmin = g < L.kwmin ? g : L.kwmin;
+        const int64_t sv = (int64_t)offs[v];
+        const int64_t wv = (sv + mis) >> 6;
+        if (wv != wu) {
+            wn = wv;
+            break;
         }
+        if ((int64_t)offs[v + 1] > sv) bits |= 1ull << ((sv + mis) & 63);
     }
-    L.sd = nd & 0x7fffu;
-    L.sk = nk & 0x7fffu;
+    bnd[wu - w0] = bits;
+    for (int64_t w = wu + 1; w < wn; ++w) bnd[w - w0] = 0;
 }
+
+__device__ __forceinline__ void scan_bot(const RulesDev& R, const uint16_t* s_td, const uint16_t* s_tk,
+                                         uint32_t& sd, uint32_t& sk, uint32_t& cnt, Event* __restrict__ evl,
+                                         uint32_t pos) {
+    const uint32_t nd = s_td[sd + (uint32_t)(R.CD - 1)];
+    const uint32_t nk = s_tk[sk + (uint32_t)(R.CK - 1)];
+    if ((nd | nk) & 0x8000u) {
+        Event e;
+        e.pos = pos;
+        e.sd = (uint16_t)sd;
+        e.sk = (uint16_t)sk;
+        evl[cnt++] = e;
+    }
+    sd = (uint32_t)R.d_start;
+    sk = (uint32_t)R.k_start;
+}
+
+#define SCAN_STEP(K, OFF)                                                                         \
+    {                                                                                             \
+        const int64_t jj = jc + (K);                                                             \
+        const uint32_t nd = s_td[sd + (cc[K] & 0xffu)];                                         \
+        const uint32_t nk = s_tk[sk + (cc[K] >> 8)];                                            \
+        if (jj >= lo && jj <= hi) {                                                               \
+            if (__builtin_expect(((nd | nk) & 0x8000u) != 0, 0)) {                                \
+                Event e;                                                                          \
+                e.pos = (uint32_t)(jj + 1 - base);                                                \
+                e.sd = (uint16_t)sd;                                                              \
+                e.sk = (uint16_t)sk;                                                              \
+                evl[cnt++] = e;                                                                   \
+            }                                                                                     \
+            sd = nd & 0x7fffu;                                                                    \
+            sk = nk & 0x7fffu;                                                                    \
+            if (__builtin_expect((bits >> ((OFF) + (K))) & 1, 0))                                 \
+                scan_bot(R, s_td, s_tk, sd, sk, cnt, evl, (uint32_t)(jj - base));                 \
+        }                                                                                         \
+    }
+
+#define SCAN_CLASSES(W)                                                                           \
+    cc[0] = s_cmap[byte_c<0>(W)];                                                                 \
+    cc[1] = s_cmap[byte_c<1>(W)];                                                                 \
+    cc[2] = s_cmap[byte_c<2>(W)];                                                                 \
+    cc[3] = s_cmap[byte_c<3>(W)];                                                                 \
+    cc[4] = s_cmap[byte_c<4>(W)];                                                                 \
+    cc[5] = s_cmap[byte_c<5>(W)];                                                                 \
+    cc[6] = s_cmap[byte_c<6>(W)];                                                                 \
+    cc[7] = s_cmap[byte_c<7>(W)];                                                                 \
+    cc[8] = s_cmap[byte_c<8>(W)];                                                                 \
+    cc[9] = s_cmap[byte_c<9>(W)];                                                                 \
+    cc[10] = s_cmap[byte_c<10>(W)];                                                               \
+    cc[11] = s_cmap[byte_c<11>(W)];                                                               \
+    cc[12] = s_cmap[byte_c<12>(W)];                                                               \
+    cc[13] = s_cmap[byte_c<13>(W)];                                                               \
+    cc[14] = s_cmap[byte_c<14>(W)];                                                               \
+    cc[15] = s_cmap[byte_c<15>(W)];
+
+#define SCAN_SUB(W, OFF)                                                                          \
+    {                                                                                             \
+        uint32_t cc[16];                                                                          \
+        SCAN_CLASSES(W)                                                                           \
+        const int64_t jc = blk * 64 - mis + (OFF);                                                \
+        SCAN_STEP(15, OFF) SCAN_STEP(14, OFF) SCAN_STEP(13, OFF) SCAN_STEP(12, OFF)               \
+        SCAN_STEP(11, OFF) SCAN_STEP(10, OFF) SCAN_STEP(9, OFF) SCAN_STEP(8, OFF)                 \
+        SCAN_STEP(7, OFF) SCAN_STEP(6, OFF) SCAN_STEP(5, OFF) SCAN_STEP(4, OFF)                   \
+        SCAN_STEP(3, OFF) SCAN_STEP(2, OFF) SCAN_STEP(1, OFF) SCAN_STEP(0, OFF)                   \
+    }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ offs, uint32_t n_utt,
-                                                     const uint8_t* __restrict__ role,
                                                      const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                     Event* __restrict__ ev, uint32_t* __restrict__ n_ev,
-                                                     int16_t* __restrict__ kw_group) {
+                                                     const uint64_t* __restrict__ bnd, Event* __restrict__ ev,
+                                                     uint32_t* __restrict__ lane_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     uint16_t* s_cmap = reinterpret_cast<uint16_t*>(smem32);
     const int nd_words = (R.SD * R.CD + 1) / 2;
@@ -155,80 +241,44 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
     __syncthreads();
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
-    const uint64_t base = offs[0];
-    const uint64_t total_end = offs[n_utt];
-    const uintptr_t lo_ok = (uintptr_t)(text + base);
-    const uintptr_t hi_ok = (uintptr_t)(text + total_end);
-    const uint32_t u1 = first_utt[c + 1];
-    for (uint32_t u = first_utt[c]; u < u1; ++u) {
-        const int64_t s = (int64_t)offs[u];
-        const int64_t e = (int64_t)offs[u + 1];
-        const bool agent = role[u] == PII_ROLE_AGENT;
-        ScanLane L;
-        L.sd = (uint32_t)R.d_start;
-        L.sk = (uint32_t)R.k_start;
-        L.cnt = 0;
-        L.kmask = agent ? 0xffffu : 0u;
-        L.kwmin = R.kw_always_min;
-        L.evu = ev + (s - (int64_t)base);
-        L.s = s;
-        int64_t j = e - 1;
-        while (j >= s) {
-            const uintptr_t a = (uintptr_t)(text + j);
-            const uintptr_t cb = a & ~(uintptr_t)15;
-            const int k_hi = (int)(a & 15);
-            const int64_t room = j - s;
-            const int k_lo = room >= k_hi ? 0 : k_hi - (int)room;
-            if (cb >= lo_ok && cb + 16 <= hi_ok) {
-                const uint4 w = *reinterpret_cast<const uint4*>(cb);
-                if (k_hi == 15 && k_lo == 0) {
-                    const int64_t j0 = j - 15;
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<15>(w), j0 + 15);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<14>(w), j0 + 14);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<13>(w), j0 + 13);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<12>(w), j0 + 12);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<11>(w), j0 + 11);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<10>(w), j0 + 10);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<9>(w), j0 + 9);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<8>(w), j0 + 8);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<7>(w), j0 + 7);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<6>(w), j0 + 6);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<5>(w), j0 + 5);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<4>(w), j0 + 4);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<3>(w), j0 + 3);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<2>(w), j0 + 2);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<1>(w), j0 + 1);
-                    scan_step(R, s_cmap, s_td, s_tk, L, byte_c<0>(w), j0 + 0);
-                } else {
-                    for (int k = k_hi; k >= k_lo; --k) scan_step(R, s_cmap, s_td, s_tk, L, byte_of(w, k), j - (k_hi - k));
-                }
-            } else {
-                for (int k = k_hi; k >= k_lo; --k) {
-                    const int64_t jj = j - (k_hi - k);
-                    scan_step(R, s_cmap, s_td, s_tk, L, text[jj], jj);
-                }
+    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
+    const int64_t base = (int64_t)offs[0];
+    const int64_t lo = (int64_t)offs[u0];   // lane range [lo, hi]
+    const int64_t hi = (int64_t)offs[u1] - 1;
+    uint32_t cnt = 0;
+    if (hi >= lo) {
+        Event* __restrict__ evl = ev + (lo - base);
+        uint32_t sd = (uint32_t)R.d_start, sk = (uint32_t)R.k_start;
+        // aligned 64-byte blocks in ADDRESS space: block b covers positions [64b - mis, 64b - mis + 64)
+        const int64_t mis = (int64_t)((uintptr_t)text & 63);
+        const uint4* __restrict__ tp = reinterpret_cast<const uint4*>(text - mis);
+        const int64_t b0 = (base + mis) >> 6;
+        const int64_t b_hi = (hi + mis) >> 6;
+        const int64_t b_lo = (lo + mis) >> 6;
+        uint4 n0 = tp[4 * b_hi], n1 = tp[4 * b_hi + 1], n2 = tp[4 * b_hi + 2], n3 = tp[4 * b_hi + 3];
+        uint64_t nb = bnd[b_hi - b0];
+        for (int64_t blk = b_hi; blk >= b_lo; --blk) {
+            const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
+            const uint64_t bits = nb;
+            if (blk > b_lo) {
+                const int64_t q = 4 * (blk - 1);
+                n0 = tp[q];
+                n1 = tp[q + 1];
+                n2 = tp[q + 2];
+                n3 = tp[q + 3];
+                nb = bnd[blk - 1 - b0];
             }
-            j -= (k_hi - k_lo + 1);
+            SCAN_SUB(w3, 48)
+            SCAN_SUB(w2, 32)
+            SCAN_SUB(w1, 16)
+            SCAN_SUB(w0, 0)
         }
-        // beginning of the utterance: the end-of-text pseudo class of the reverse automata
-        {
-            const uint32_t nd = s_td[L.sd + (uint32_t)(R.CD - 1)];
-            const uint32_t nk = s_tk[L.sk + (uint32_t)(R.CK - 1)];
-            if (nd & 0x8000u) {
-                Event evt;
-                evt.pos = 0;
-                evt.acc = R.d_accid[L.sd + (uint32_t)(R.CD - 1)];
-                L.evu[L.cnt++] = evt;
-            }
-            if (nk & L.kmask & 0x8000u) {
-                const int g = R.k_acc_min[R.k_accid[L.sk + (uint32_t)(R.CK - 1)]];
-                L.kwmin = g < L.kwmin ? g : L.kwmin;
-            }
-        }
-        n_ev[u] = L.cnt;
-        kw_group[u] = (int16_t)((agent && L.kwmin != KW_NONE) ? L.kwmin : -1);
     }
+    lane_cnt[c] = cnt;
 }
+#undef SCAN_STEP
+#undef SCAN_CLASSES
+#undef SCAN_SUB
 
 // ---------------------------------------------------------------------------- context (a11)
 // segmented (by conversation run) scan of "latest agent row with a context hit"
@@ -353,115 +403,340 @@ __global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int16_t* _
     }
 }
 
-// ---------------------------------------------------------------------------------- k_resolve
-__global__ __launch_bounds__(256) void k_resolve(const RulesDev R, const uint8_t* __restrict__ text,
-                                                 const uint64_t* __restrict__ offs, uint32_t n_utt,
-                                                 const uint8_t* __restrict__ role, const int16_t* __restrict__ ctx,
-                                                 const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev,
-                                                 pii_span* __restrict__ fd, uint32_t* __restrict__ n_find,
-                                                 uint32_t* __restrict__ out_len) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n_utt) return;
-    const uint64_t base = offs[0];
-    const uint64_t s_abs = offs[u], e_abs = offs[u + 1];
-    const int L = (int)(e_abs - s_abs);
-    const uint8_t* t0 = text + s_abs;
-    const uint32_t ne = n_ev[u];
-    const Event* evu = ev + (s_abs - base);
-    pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
-    const int v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
-    const int T = R.T;
-    const int minlik = R.var_minlik[v];
-    uint32_t cur[P_MAX];
-    uint64_t touched = 0;
-    int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
-    uint32_t ex_valid = 0;
-    int max_end = 0;
-    uint32_t nf = 0;
-    int64_t out = L;
-    for (int k = (int)ne - 1; k >= 0; --k) {
-        const Event E = evu[k];
-        const int s = (int)E.pos;
-        const uint32_t a0 = R.d_acc_off[E.acc], a1 = R.d_acc_off[E.acc + 1];
-        int best_e = -1, best_t = 0, best_lik = 0;
-        for (uint32_t i = a0; i < a1; ++i) {
-            const int p = R.d_acc_ids[i];
-            const int t = R.det_type[p];
-            if (!R.var_enabled[v * T + t]) continue;
-            if (((touched >> p) & 1) && (uint32_t)s < cur[p]) continue;
-            const int e = first_run(R.pool, R.first_desc + 8 * p, t0, s, L);
-            if (e < 0) continue;
-            cur[p] = (uint32_t)e;
-            touched |= 1ull << p;
-            const int xi = R.det_exidx[p];
-            if (!validate(R.det_val[p], t0 + s, e - s)) {
-                if (xi != 0xff) ex_valid &= ~(1u << xi);
-                continue;
+// ---------------------------------------------------------------------------------- resolve
+// The sparse phase is data-parallel: divergent per-utterance loops serialise a wavefront, so the work
+// is split into uniform phases over a queue of (candidate start, pattern) PAIRS.
+//   k_pairs      per scan lane: decode its events; context keyword group of AGENT rows; append one
+//                pair per (D event, pattern in the accept set) -- the lane's block is written back to
+//                front so it ends up ascending by start, accept-set order within a start
+//   k_pair_first per pair: anchored leftmost-first run -> end (or -1)      [lockstep DFA runs]
+//   k_pair_eval  per matched pair: validator + hotword windows of the row's context variant -> likelihood
+//   k_select     per scan lane: finditer skipping, exclusion, overlap resolution -> kept findings
+struct Pair {
+    uint32_t u;     // utterance
+    uint32_t s;     // start, relative to the utterance
+    uint16_t p;     // detector pattern
+    int16_t lik;    // likelihood after validation + hotwords; -1 = invalid
+    int32_t e;      // leftmost-first end, -1 = no match
+};
+enum RB {
+    RB_PTRANS, RB_PFLAGS, RB_PCMAP, RB_FDESC, RB_HDESC, RB_HRULE, RB_DTYPE, RB_DVAL, RB_DLIK, RB_DEX,
+    RB_VEN, RB_VMIN, RB_ROFF, RB_RIDS, RB_XOFF, RB_XIDS, RB_TOKOFF, RB_AOFF, RB_AIDS, RB_CMAP2, RB_N
+};
+struct RBOffs {
+    uint32_t off[RB_N];
+    uint32_t total;   // bytes, multiple of 16
+};
+
+__global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint8_t* __restrict__ text,
+                                               const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
+                                               uint32_t n_chunks, const Event* __restrict__ ev,
+                                               const uint32_t* __restrict__ lane_cnt, const uint8_t* __restrict__ role,
+                                               int16_t* __restrict__ kw, Pair* __restrict__ pairs, uint64_t pair_cap,
+                                               unsigned long long* __restrict__ pair_count,
+                                               uint64_t* __restrict__ lane_pair, uint32_t* __restrict__ lane_np,
+                                               uint32_t* __restrict__ err) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool valid = c < n_chunks;
+    const uint32_t cnt = valid ? lane_cnt[c] : 0u;
+    const int64_t base = (int64_t)offs[0];
+    const Event* evl = nullptr;
+    int64_t u_top = 0;
+    if (cnt) {
+        const uint32_t u0 = first_utt[c];
+        evl = ev + ((int64_t)offs[u0] - base);
+        u_top = (int64_t)first_utt[c + 1] - 1;
+    }
+    // pass 1: count pairs, keyword groups
+    uint32_t np = 0;
+    {
+        int64_t u = u_top;
+        int64_t s_u = cnt ? (int64_t)offs[u] - base : 0;
+        bool agent = cnt ? role[u] == PII_ROLE_AGENT : false;
+        int g = KW_NONE;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const Event E = evl[k];
+            const int64_t pos = E.pos;
+            while (pos < s_u) {
+                if (g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
+                g = KW_NONE;
+                --u;
+                s_u = (int64_t)offs[u] - base;
+                agent = role[u] == PII_ROLE_AGENT;
             }
-            int lik = R.det_lik[p];
-            const uint32_t r0 = R.rule_off[v * T + t], r1 = R.rule_off[v * T + t + 1];
+            const uint32_t cc = pos == s_u ? 0xffffffffu : (uint32_t)R.cmap2[text[base + pos - 1]];
+            const uint32_t cd = pos == s_u ? (uint32_t)(R.CD - 1) : (cc & 0xffu);
+            const uint32_t acc = R.d_accid[E.sd + cd];
+            np += R.d_acc_off[acc + 1] - R.d_acc_off[acc];
+            if (agent) {
+                const uint32_t ck = pos == s_u ? (uint32_t)(R.CK - 1) : (cc >> 8);
+                const uint32_t a = R.k_accid[E.sk + ck];
+                if (a) g = min(g, (int)R.k_acc_min[a]);
+            }
+        }
+        if (cnt && g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
+    }
+    // wave-aggregated allocation
+    uint32_t incl = np;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    unsigned long long wbase = 0;
+    if (lane == 63 && incl) wbase = atomicAdd(pair_count, (unsigned long long)incl);
+    wbase = __shfl(wbase, 63);
+    const uint64_t my = wbase + (incl - np);
+    if (valid) {
+        lane_pair[c] = my;
+        lane_np[c] = np;
+    }
+    if (np == 0) return;
+    if (my + np > pair_cap) {
+        atomicOr(err, (uint32_t)ERR_QUEUE);
+        return;
+    }
+    // pass 2: write back to front -> ascending by start
+    uint64_t w = my + np;
+    int64_t u = u_top;
+    int64_t s_u = (int64_t)offs[u] - base;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const Event E = evl[k];
+        const int64_t pos = E.pos;
+        while (pos < s_u) {
+            --u;
+            s_u = (int64_t)offs[u] - base;
+        }
+        const uint32_t cd = pos == s_u ? (uint32_t)(R.CD - 1) : (uint32_t)(R.cmap2[text[base + pos - 1]] & 0xffu);
+        const uint32_t acc = R.d_accid[E.sd + cd];
+        const uint32_t a0 = R.d_acc_off[acc], a1 = R.d_acc_off[acc + 1];
+        w -= a1 - a0;
+        for (uint32_t i = a0; i < a1; ++i) {
+            Pair P;
+            P.u = (uint32_t)u;
+            P.s = (uint32_t)(pos - s_u);
+            P.p = R.d_acc_ids[i];
+            P.lik = -1;
+            P.e = -1;
+            pairs[w + (i - a0)] = P;
+        }
+    }
+}
+
+__device__ __forceinline__ const uint8_t* load_rblob(const uint4* __restrict__ rblob, const RBOffs& ro, uint4* lds4) {
+    for (uint32_t i = threadIdx.x; i < ro.total / 16; i += blockDim.x) lds4[i] = rblob[i];
+    __syncthreads();
+    return reinterpret_cast<const uint8_t*>(lds4);
+}
+
+__global__ __launch_bounds__(1024) void k_pair_first(const uint4* __restrict__ rblob, const RBOffs ro,
+                                                     const uint8_t* __restrict__ text,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const unsigned long long* __restrict__ pair_count,
+                                                     uint64_t pair_cap, Pair* __restrict__ pairs) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    const uint8_t* lb = load_rblob(rblob, ro, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + ro.off[RB_PTRANS]), lb + ro.off[RB_PFLAGS],
+                    lb + ro.off[RB_PCMAP]};
+    const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + ro.off[RB_FDESC]);
+    const uint64_t n = min((uint64_t)*pair_count, pair_cap);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        Pair P = pairs[i];
+        const uint64_t sa = offs[P.u];
+        const int L = (int)(offs[P.u + 1] - sa);
+        P.e = first_run(pool, fdesc + 8 * P.p, text + sa, (int)P.s, L);
+        pairs[i].e = P.e;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_pair_eval(const RulesDev R, const uint4* __restrict__ rblob, const RBOffs ro,
+                                                    const uint8_t* __restrict__ text,
+                                                    const uint64_t* __restrict__ offs,
+                                                    const uint8_t* __restrict__ role, const int16_t* __restrict__ ctx,
+                                                    const unsigned long long* __restrict__ pair_count,
+                                                    uint64_t pair_cap, Pair* __restrict__ pairs) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    const uint8_t* lb = load_rblob(rblob, ro, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + ro.off[RB_PTRANS]), lb + ro.off[RB_PFLAGS],
+                    lb + ro.off[RB_PCMAP]};
+    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + ro.off[RB_HDESC]);
+    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + ro.off[RB_HRULE]);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + ro.off[RB_DTYPE]);
+    const uint8_t* dval = lb + ro.off[RB_DVAL];
+    const uint8_t* dlik = lb + ro.off[RB_DLIK];
+    const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + ro.off[RB_ROFF]);
+    const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + ro.off[RB_RIDS]);
+    const int T = R.T;
+    const uint64_t n = min((uint64_t)*pair_count, pair_cap);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const Pair P = pairs[i];
+        if (P.e < 0) continue;
+        const uint64_t sa = offs[P.u];
+        const int L = (int)(offs[P.u + 1] - sa);
+        const uint8_t* t0 = text + sa;
+        const int s = (int)P.s, e = P.e;
+        int lik = -1;
+        if (validate(dval[P.p], t0 + s, e - s)) {
+            const int v = (role[P.u] == PII_ROLE_CUSTOMER && ctx[P.u] >= 0) ? ctx[P.u] + 1 : 0;
+            const int t = dtype[P.p];
+            lik = dlik[P.p];
+            const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
             for (uint32_t q = r0; q < r1; ++q) {
-                const int h = R.rule_ids[q];
-                const int wb = R.hot_rule[4 * h], wa = R.hot_rule[4 * h + 1];
-                const int fixed = R.hot_rule[4 * h + 2], rel = R.hot_rule[4 * h + 3];
+                const int h = rids[q];
+                const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
+                const int fixed = hrule[4 * h + 2], rel = hrule[4 * h + 3];
                 bool hit = false;
-                if (wb > 0) hit = hot_run(R.pool, R.hot_desc + 8 * h, t0, s - wb > 0 ? s - wb : 0, s);
-                if (!hit && wa > 0) hit = hot_run(R.pool, R.hot_desc + 8 * h, t0, e, e + wa < L ? e + wa : L);
+                if (wb > 0) hit = hot_run(pool, hdesc + 8 * h, t0, s - wb > 0 ? s - wb : 0, s);
+                if (!hit && wa > 0) hit = hot_run(pool, hdesc + 8 * h, t0, e, e + wa < L ? e + wa : L);
                 if (hit) {
-                    if (fixed) lik = fixed;
-                    else {
+                    if (fixed) {
+                        lik = fixed;
+                    } else {
                         lik += rel;
                         lik = lik < 1 ? 1 : (lik > 5 ? 5 : lik);
                     }
                 }
             }
-            if (lik < minlik) {
-                if (xi != 0xff) ex_valid &= ~(1u << xi);
-                continue;
-            }
-            if (xi != 0xff) {
-                ex_s[xi] = s;
-                ex_e[xi] = e;
-                ex_t[xi] = t;
-                ex_valid |= 1u << xi;
-            }
-            // exclusion (FULL_MATCH): inside a finding of an excluded type (A.5)
-            const uint32_t x0 = R.excl_off[v * T + t], x1 = R.excl_off[v * T + t + 1];
-            bool excluded = false;
-            for (uint32_t q = x0; q < x1 && !excluded; ++q) {
-                const int xt = R.excl_ids[q];
-                for (int x = 0; x < R.NE; ++x) {
-                    if (x == xi || !((ex_valid >> x) & 1) || ex_t[x] != xt) continue;
-                    if (ex_s[x] <= s && e <= ex_e[x]) {
-                        excluded = true;
-                        break;
+        }
+        pairs[i].lik = (int16_t)lik;
+    }
+}
+
+constexpr int LIVE = 8;            // register-resident "previous match end" slots per lane
+
+__global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint64_t* __restrict__ offs,
+                                                uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
+                                                const uint32_t* __restrict__ lane_np, const Pair* __restrict__ pairs,
+                                                uint64_t pair_cap, const uint8_t* __restrict__ role,
+                                                const int16_t* __restrict__ ctx, pii_span* __restrict__ fd,
+                                                uint32_t* __restrict__ n_find, uint32_t* __restrict__ out_len) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    const uint32_t np = lane_np[c];
+    if (np == 0 || lane_pair[c] + np > pair_cap) return;     // overflowed queue: the batch is re-run
+    const Pair* pl = pairs + lane_pair[c];
+    const int64_t base = (int64_t)offs[0];
+    const int T = R.T;
+    uint32_t i = 0;
+    while (i < np) {
+        const uint32_t u = pl[i].u;
+        const int64_t s_abs = (int64_t)offs[u];
+        const int L = (int)((int64_t)offs[u + 1] - s_abs);
+        const int v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
+        const int minlik = R.var_minlik[v];
+        pii_span* fdu = fd + (s_abs - base) / R.min_len;
+        int lp[LIVE], le[LIVE];
+#pragma unroll
+        for (int q = 0; q < LIVE; ++q) {
+            lp[q] = -1;
+            le[q] = -1;
+        }
+        uint32_t cur_s[P_MAX];     // spill array: touched only when LIVE slots overflow
+        bool spilled = false;
+        int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
+        uint32_t ex_valid = 0;
+        int max_end = 0;
+        uint32_t nf = 0;
+        int64_t out = L;
+        while (i < np && pl[i].u == u) {
+            const int s = (int)pl[i].s;
+            int best_e = -1, best_t = 0, best_lik = 0;
+            for (; i < np && pl[i].u == u && (int)pl[i].s == s; ++i) {
+                const Pair P = pl[i];
+                const int p = P.p;
+                const int t = R.det_type[p];
+                if (!R.var_enabled[v * T + t]) continue;
+                int prev_end = -1;
+                if (spilled) {
+                    prev_end = (int)cur_s[p];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < LIVE; ++q)
+                        if (lp[q] == p) prev_end = le[q];
+                }
+                if (s < prev_end) continue;               // inside p's previous match (finditer)
+                const int e = P.e;
+                if (e < 0) continue;
+                if (spilled) {
+                    cur_s[p] = (uint32_t)e;
+                } else {
+                    int slot = -1;
+#pragma unroll
+                    for (int q = 0; q < LIVE; ++q)
+                        if (lp[q] == p) slot = q;
+                    if (slot < 0) {
+#pragma unroll
+                        for (int q = 0; q < LIVE; ++q)
+                            if (slot < 0 && le[q] <= s) slot = q;
+                    }
+                    if (slot >= 0) {
+#pragma unroll
+                        for (int q = 0; q < LIVE; ++q)
+                            if (q == slot) {
+                                lp[q] = p;
+                                le[q] = e;
+                            }
+                    } else {
+                        for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
+#pragma unroll
+                        for (int q = 0; q < LIVE; ++q)
+                            if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
+                        cur_s[p] = (uint32_t)e;
+                        spilled = true;
                     }
                 }
+                const int xi = R.det_exidx[p];
+                const int lik = P.lik;
+                if (lik < minlik) {                        // invalid (-1) or below min_likelihood
+                    if (xi != 0xff) ex_valid &= ~(1u << xi);
+                    continue;
+                }
+                if (xi != 0xff) {
+#pragma unroll
+                    for (int x = 0; x < NE_MAX; ++x)
+                        if (x == xi) {
+                            ex_s[x] = s;
+                            ex_e[x] = e;
+                            ex_t[x] = t;
+                        }
+                    ex_valid |= 1u << xi;
+                }
+                const uint32_t x0 = R.excl_off[v * T + t], x1 = R.excl_off[v * T + t + 1];
+                bool excluded = false;
+                for (uint32_t q = x0; q < x1; ++q) {
+                    const int xt = R.excl_ids[q];
+#pragma unroll
+                    for (int x = 0; x < NE_MAX; ++x)
+                        if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
+                            excluded = true;
+                }
+                if (excluded) continue;
+                const bool better = best_e < 0 || e > best_e ||
+                                    (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
+                if (better) {
+                    best_e = e;
+                    best_t = t;
+                    best_lik = lik;
+                }
             }
-            if (excluded) continue;
-            // best at this start: longest, then most likely, then lowest type index (A.6)
-            const bool better = best_e < 0 || e > best_e || (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
-            if (better) {
-                best_e = e;
-                best_t = t;
-                best_lik = lik;
+            if (best_e >= 0 && s >= max_end) {
+                pii_span f;
+                f.utt = u;
+                f.start = (uint32_t)s;
+                f.end = (uint32_t)best_e;
+                f.info_type = (uint16_t)best_t;
+                f.likelihood = (uint8_t)best_lik;
+                f.flags = 0;
+                fdu[nf++] = f;
+                max_end = best_e;
+                out += (int64_t)(R.tok_off[best_t + 1] - R.tok_off[best_t]) - (best_e - s);
             }
         }
-        if (best_e >= 0 && s >= max_end) {
-            pii_span f;
-            f.utt = u;
-            f.start = (uint32_t)s;
-            f.end = (uint32_t)best_e;
-            f.info_type = (uint16_t)best_t;
-            f.likelihood = (uint8_t)best_lik;
-            f.flags = 0;
-            fdu[nf++] = f;
-            max_end = best_e;
-            out += (int64_t)(R.tok_off[best_t + 1] - R.tok_off[best_t]) - (best_e - s);
+        if (nf) {
+            n_find[u] = nf;
+            out_len[u] = (uint32_t)out;
         }
     }
-    n_find[u] = nf;
-    out_len[u] = (uint32_t)out;
 }
 
 // ---------------------------------------------------------------------------- exclusive scans
@@ -556,20 +831,49 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 
 __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t* __restrict__ span_offs,
                            uint32_t n_utt, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
-                           uint64_t* __restrict__ totals) {
+                           uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count) {
     const uint64_t ob = out_offs[n_utt], ns = span_offs[n_utt];
     if (ob > out_cap || ns > span_cap) atomicOr(err, (uint32_t)ERR_CAPACITY);
     totals[0] = ob;
     totals[1] = ns;
     totals[2] = *err;
+    totals[3] = *pair_count;
 }
 
 // ---------------------------------------------------------------------------------- k_redact
-// one wavefront per utterance: copy kept byte runs and "[INFO_TYPE]" tokens to the prefix-summed
-// output position; emit spans; per-type histogram through LDS.
+// Prefix-sum scatter.  A workgroup owns the utterances starting in REDACT_TILE_CHUNKS scan chunks:
+// one contiguous input range and one contiguous output range.  It stages the input bytes and the
+// "[INFO_TYPE]" token strings in LDS and builds a PIECE table (copy runs and tokens, sorted by output
+// offset; 1 + 2*findings pieces per utterance).  Every lane then assembles aligned 16-byte OUTPUT
+// blocks from LDS through the piece table -- one uniform code path -- and stores each with a single
+// dwordx4 store; only the two partial blocks at the range edges use byte stores.  Tiles that do not
+// fit fall back to a wavefront-per-utterance copy.
 constexpr int REDACT_BLOCK = 256;
+constexpr int REDACT_TILE_CHUNKS = 16;
+constexpr int STAGE_MAX = 16 * 1024;
+constexpr int TILE_UTT_MAX = 512;
+constexpr int PIECE_MAX = 1536;
+constexpr int TOK_MAX = 2048;
+
+__device__ uint32_t redact_byte_slow(const RulesDev& R, const uint8_t* src, const pii_span* fdu, uint32_t nf,
+                                     uint32_t rel) {
+    uint32_t pin = 0, pout = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+        const pii_span F = fdu[f];
+        const uint32_t run = F.start - pin;
+        if (rel < pout + run) return src[pin + (rel - pout)];
+        pout += run;
+        const uint32_t t0 = R.tok_off[F.info_type], tl = R.tok_off[F.info_type + 1] - t0;
+        if (rel < pout + tl) return R.tok_bytes[t0 + (rel - pout)];
+        pout += tl;
+        pin = F.end;
+    }
+    return src[pin + (rel - pout)];
+}
+
 __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ offs, uint32_t n_utt,
+                                                         const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
                                                          const pii_span* __restrict__ fd,
                                                          const uint32_t* __restrict__ n_find,
                                                          const uint64_t* __restrict__ out_offs,
@@ -577,43 +881,173 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
                                                          const uint32_t* __restrict__ err, uint8_t* __restrict__ out,
                                                          pii_span* __restrict__ spans,
                                                          unsigned long long* __restrict__ hist) {
+    __shared__ __attribute__((aligned(16))) uint4 s_buf4[(STAGE_MAX + TOK_MAX) / 16 + 2];
+    __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (tile relative)
+    __shared__ uint32_t s_psrc[PIECE_MAX + 1];     // piece source offset in s_buf
+    __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
     __shared__ uint32_t sh_hist[256];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) sh_hist[i] = 0;
+    __shared__ int s_staged;
+    if (*err != 0) return;
+    const uint32_t c0 = blockIdx.x * REDACT_TILE_CHUNKS;
+    const uint32_t c1 = min(c0 + REDACT_TILE_CHUNKS, n_chunks);
+    const uint32_t u0 = first_utt[c0], u1 = first_utt[c1];
+    if (u0 >= u1) return;
+    const uint32_t nu = u1 - u0;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < 256; i += REDACT_BLOCK) sh_hist[i] = 0;
+    const uint64_t base = offs[0];
+    const int64_t in_lo = (int64_t)offs[u0], in_hi = (int64_t)offs[u1];
+    const int64_t out_lo = (int64_t)out_offs[u0], out_hi = (int64_t)out_offs[u1];
+    const int64_t mis = (int64_t)((uintptr_t)text & 15);
+    const int64_t a_lo = (in_lo + mis) >> 4;
+    const int64_t a_hi = in_hi > in_lo ? (in_hi - 1 + mis) >> 4 : a_lo;
+    const int64_t stage_pos = a_lo * 16 - mis;          // text position of s_buf[0]
+    const uint32_t tok_at = (uint32_t)((a_hi - a_lo + 1) * 16);
+    const uint32_t tok_len = R.tok_off[R.T];
+    bool staged = tok_at <= STAGE_MAX && tok_len <= TOK_MAX && nu <= TILE_UTT_MAX;
+    uint8_t* s_buf = reinterpret_cast<uint8_t*>(s_buf4);
+    // ---- piece counts + block scan ----
+    uint32_t cnt_i[2] = {0, 0};
+    if (staged) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t i = tid * 2 + r;
+            cnt_i[r] = i < nu ? 1 + 2 * n_find[u0 + i] : 0;
+        }
+    }
+    uint32_t tsum = cnt_i[0] + cnt_i[1];
+    uint32_t incl = tsum;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
     __syncthreads();
-    const bool ok = *err == 0;
-    const int lane = threadIdx.x & 63;
-    const uint32_t u = blockIdx.x * (REDACT_BLOCK / 64) + (threadIdx.x >> 6);
-    if (ok && u < n_utt) {
-        const uint64_t base = offs[0];
-        const uint64_t s_abs = offs[u], e_abs = offs[u + 1];
-        const uint8_t* src = text + s_abs;
-        const uint32_t nf = n_find[u];
-        const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
-        uint8_t* dst = out + out_offs[u];
-        pii_span* sp = spans + span_offs[u];
-        uint32_t pos = 0;
-        uint64_t o = 0;
-        for (uint32_t f = 0; f < nf; ++f) {
-            const pii_span F = fdu[f];
-            for (uint32_t i = lane; i < F.start - pos; i += 64) dst[o + i] = src[pos + i];
-            o += F.start - pos;
-            const uint32_t t0 = R.tok_off[F.info_type], tl = R.tok_off[F.info_type + 1] - t0;
-            for (uint32_t i = lane; i < tl; i += 64) dst[o + i] = R.tok_bytes[t0 + i];
-            o += tl;
-            pos = F.end;
-            if (lane == 0) {
-                sp[f] = F;
-                if (F.info_type < 256) atomicAdd(&sh_hist[F.info_type], 1u);
+    uint32_t wpre = 0, total_p = 0;
+    for (int w = 0; w < REDACT_BLOCK / 64; ++w) {
+        if (w < wid) wpre += s_wsum[w];
+        total_p += s_wsum[w];
+    }
+    if (tid == 0) s_staged = staged && total_p <= PIECE_MAX;
+    __syncthreads();
+    staged = s_staged;
+    if (staged) {
+        const uint4* __restrict__ tp = reinterpret_cast<const uint4*>(text - mis);
+        for (int64_t a = a_lo + tid; a <= a_hi; a += REDACT_BLOCK) s_buf4[a - a_lo] = tp[a];
+        for (uint32_t i = tid; i < tok_len; i += REDACT_BLOCK) s_buf[tok_at + i] = R.tok_bytes[i];
+        uint32_t pb = wpre + incl - tsum;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t i = tid * 2 + r;
+            if (i < nu) {
+                const uint32_t u = u0 + i;
+                const uint32_t nf = cnt_i[r] >> 1;
+                const uint32_t so = (uint32_t)((int64_t)offs[u] - stage_pos);
+                uint32_t po = (uint32_t)((int64_t)out_offs[u] - out_lo);
+                if (nf == 0) {
+                    s_pout[pb] = po;
+                    s_psrc[pb] = so;
+                    ++pb;
+                } else {
+                    const pii_span* fdu = fd + (offs[u] - base) / (uint64_t)R.min_len;
+                    uint32_t pin = 0;
+                    for (uint32_t f = 0; f < nf; ++f) {
+                        const pii_span F = fdu[f];
+                        s_pout[pb] = po;
+                        s_psrc[pb] = so + pin;
+                        po += F.start - pin;
+                        ++pb;
+                        const uint32_t t0 = R.tok_off[F.info_type];
+                        s_pout[pb] = po;
+                        s_psrc[pb] = tok_at + t0;
+                        po += R.tok_off[F.info_type + 1] - t0;
+                        ++pb;
+                        pin = F.end;
+                    }
+                    s_pout[pb] = po;
+                    s_psrc[pb] = so + pin;
+                    ++pb;
+                }
             }
         }
-        const uint32_t L = (uint32_t)(e_abs - s_abs);
-        for (uint32_t i = lane; i < L - pos; i += 64) dst[o + i] = src[pos + i];
+        if (tid == 0) s_pout[total_p] = (uint32_t)(out_hi - out_lo);   // sentinel
     }
     __syncthreads();
-    if (ok) {
-        for (int i = threadIdx.x; i < R.T && i < 256; i += blockDim.x)
-            if (sh_hist[i]) atomicAdd(&hist[i], (unsigned long long)sh_hist[i]);
+    if (staged) {
+        const int64_t omis = (int64_t)((uintptr_t)out & 15);
+        uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
+        const int64_t q_lo = (out_lo + omis) >> 4;
+        const int64_t q_hi = out_hi > out_lo ? (out_hi - 1 + omis) >> 4 : q_lo - 1;
+        const int64_t span = out_hi - out_lo;
+        for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
+            const int64_t r0 = q * 16 - omis - out_lo;
+            const uint32_t rs = (uint32_t)(r0 > 0 ? r0 : 0);
+            // last piece with s_pout <= rs
+            uint32_t lo_i = 0, hi_i = total_p - 1;
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                if (s_pout[mid] <= rs) lo_i = mid;
+                else hi_i = mid - 1;
+            }
+            uint32_t pi = lo_i;
+            uint32_t pstart = s_pout[pi], pend = s_pout[pi + 1], psrc = s_psrc[pi];
+            uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int64_t r = r0 + k;
+                uint32_t b = 0;
+                if (r >= 0 && r < span) {
+                    while ((uint32_t)r >= pend) {
+                        ++pi;
+                        pstart = pend;
+                        pend = s_pout[pi + 1];
+                        psrc = s_psrc[pi];
+                    }
+                    b = s_buf[psrc + ((uint32_t)r - pstart)];
+                }
+                w[k >> 2] |= b << (8 * (k & 3));
+            }
+            if (r0 >= 0 && r0 + 16 <= span) {
+                op[q] = make_uint4(w[0], w[1], w[2], w[3]);
+            } else {
+                uint8_t* ob = out - omis + q * 16;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int64_t r = r0 + k;
+                    if (r >= 0 && r < span) ob[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+                }
+            }
+        }
+    } else {
+        // oversized tile: one wavefront per utterance, byte-granular
+        for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
+            const uint32_t u = u0 + i;
+            const uint64_t s_abs = offs[u];
+            const uint8_t* src = text + s_abs;
+            const uint32_t nf = n_find[u];
+            const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
+            uint8_t* dst = out + out_offs[u];
+            const uint32_t olen = (uint32_t)(out_offs[u + 1] - out_offs[u]);
+            for (uint32_t rel = lane; rel < olen; rel += 64)
+                dst[rel] = (uint8_t)(nf ? redact_byte_slow(R, src, fdu, nf, rel) : src[rel]);
+        }
     }
+    // spans + per-type histogram (findings are rare: one lane per utterance)
+    for (uint32_t i = tid; i < nu; i += REDACT_BLOCK) {
+        const uint32_t u = u0 + i;
+        const uint32_t nf = n_find[u];
+        if (nf == 0) continue;
+        const pii_span* fdu = fd + (offs[u] - base) / (uint64_t)R.min_len;
+        pii_span* sp = spans + span_offs[u];
+        for (uint32_t f = 0; f < nf; ++f) {
+            const pii_span F = fdu[f];
+            sp[f] = F;
+            if (F.info_type < 256) atomicAdd(&sh_hist[F.info_type], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < R.T && i < 256; i += REDACT_BLOCK)
+        if (sh_hist[i]) atomicAdd(&hist[i], (unsigned long long)sh_hist[i]);
 }
 
 __global__ void k_noop() {}
@@ -667,6 +1101,9 @@ struct pii_engine {
     uint32_t n_slots = 0;
     int64_t ttl_us = 0;
     size_t scan_lds = 0;
+    void* d_rblob = nullptr;
+    RBOffs ro{};
+    int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
     int64_t* st_ts = nullptr;
@@ -680,6 +1117,29 @@ struct pii_engine {
     pii_span* fd = nullptr;
     uint32_t *n_ev = nullptr, *n_find = nullptr, *out_len = nullptr, *incl = nullptr, *agg_f = nullptr;
     uint32_t* first_utt = nullptr;
+    uint32_t* lane_cnt = nullptr;
+    uint64_t* bnd = nullptr;
+    Pair* pairs = nullptr;
+    uint64_t pair_cap = 0;
+    unsigned long long* pair_count = nullptr;
+    uint64_t* lane_pair = nullptr;
+    uint32_t* lane_np = nullptr;
+    struct Call {
+        const uint8_t* text;
+        const uint64_t* offs;
+        uint32_t n_utt;
+        uint64_t total;
+        const uint32_t* slot;
+        const uint8_t* role;
+        const int64_t* ts;
+        uint8_t* out;
+        uint64_t out_cap;
+        uint64_t* out_offs;
+        pii_span* spans;
+        uint32_t span_cap;
+        int16_t* ctx_info;
+        hipStream_t st;
+    } last{};
     int16_t *kw = nullptr, *ctx = nullptr;
     int32_t *agg_v = nullptr, *commit = nullptr;
     uint64_t *span_offs = nullptr, *bsum = nullptr, *out_offs_tmp = nullptr;
@@ -729,6 +1189,10 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
         if ((rc = grow(e, e->ev, nb + 1))) return rc;
         if ((rc = grow(e, e->fd, nb / e->R.min_len + 2))) return rc;
         if ((rc = grow(e, e->first_utt, nb / BYTES_PER_LANE + 2))) return rc;
+        if ((rc = grow(e, e->lane_cnt, nb / BYTES_PER_LANE + 2))) return rc;
+        if ((rc = grow(e, e->bnd, nb / 64 + 4))) return rc;
+        if ((rc = grow(e, e->lane_pair, nb / BYTES_PER_LANE + 2))) return rc;
+        if ((rc = grow(e, e->lane_np, nb / BYTES_PER_LANE + 2))) return rc;
         e->cap_bytes = nb;
     }
     if (n_utt > e->cap_utt) {
@@ -769,23 +1233,30 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                  uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info, hipStream_t st) {
     int rc = ensure_scratch(e, n_utt, total_bytes);
     if (rc) return rc;
+    if (e->pair_cap < total_bytes / 16 + 4096) {
+        const uint64_t cap = total_bytes / 16 + 4096;
+        if ((rc = grow(e, e->pairs, cap))) return rc;
+        e->pair_cap = cap;
+    }
+    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
+                               ctx_info, st};
     const RulesDev& R = e->R;
+    int16_t* ctx = ctx_info ? ctx_info : e->ctx;
     e->epoch += 1;
     HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
     HIPCHK(hipEventRecord(e->tev[0], st));
     const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
     if (n_utt > 0) {
-        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, n_utt, n_chunks, e->first_utt);
-        if (n_chunks > 0)
+        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, R.kw_always_min,
+                                                                e->first_utt, e->out_len, e->n_find, e->kw);
+        if (n_chunks > 0) {
+            k_bounds<<<(n_utt + 255) / 256, 256, 0, st>>>(offs, n_utt, (int64_t)((uintptr_t)text & 63), e->bnd);
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
-                R, text, offs, n_utt, role, e->first_utt, n_chunks, e->ev, e->n_ev, e->kw);
-        else
-            HIPCHK(hipMemsetAsync(e->n_ev, 0, n_utt * sizeof(uint32_t), st));
-        if (n_chunks == 0) {
-            // all rows empty: no scan ran, so fill keyword results directly
-            std::vector<int16_t> none(n_utt, -1);
-            HIPCHK(hipMemcpyAsync(e->kw, none.data(), n_utt * sizeof(int16_t), hipMemcpyHostToDevice, st));
-            HIPCHK(hipStreamSynchronize(st));
+                R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->ev, e->lane_cnt);
+            k_pairs<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, text, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt,
+                                                           role, e->kw, e->pairs, e->pair_cap, e->pair_count,
+                                                           e->lane_pair, e->lane_np, e->d_err);
         }
         HIPCHK(hipGetLastError());
     }
@@ -795,31 +1266,40 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         k_ctx_scan<<<nblk, CTX_BLOCK, 0, st>>>(slot, role, e->kw, n_utt, e->n_slots, e->incl, e->agg_v, e->agg_f,
                                                e->stamp, e->epoch, e->d_err);
         k_ctx_apply<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, role, e->kw, ts, n_utt, e->n_slots, e->ttl_us,
-                                                         e->incl, e->agg_v, e->agg_f, e->st_group, e->st_ts,
-                                                         ctx_info ? ctx_info : e->ctx, e->commit);
+                                                         e->incl, e->agg_v, e->agg_f, e->st_group, e->st_ts, ctx,
+                                                         e->commit);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
-    if (n_utt > 0) {
-        k_resolve<<<(n_utt + 255) / 256, 256, 0, st>>>(R, text, offs, n_utt, role, ctx_info ? ctx_info : e->ctx,
-                                                      e->ev, e->n_ev, e->fd, e->n_find, e->out_len);
+    if (n_utt > 0 && n_chunks > 0) {
+        const uint4* rb = static_cast<const uint4*>(e->d_rblob);
+        k_pair_first<<<e->n_cu * 2, 1024, e->ro.total, st>>>(rb, e->ro, text, offs, e->pair_count, e->pair_cap,
+                                                             e->pairs);
+        k_pair_eval<<<e->n_cu * 2, 1024, e->ro.total, st>>>(R, rb, e->ro, text, offs, role, ctx, e->pair_count,
+                                                            e->pair_cap, e->pairs);
+        k_select<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, offs, n_chunks, e->lane_pair, e->lane_np, e->pairs,
+                                                         e->pair_cap, role,
+                                                         ctx, e->fd, e->n_find, e->out_len);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[3], st));
     if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
     if ((rc = exclusive_scan(e, e->n_find, n_utt, e->span_offs, st))) return rc;
-    k_finalize<<<1, 1, 0, st>>>(out_offs, e->span_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals);
+    k_finalize<<<1, 1, 0, st>>>(out_offs, e->span_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
+                                e->pair_count);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
-        k_redact<<<(n_utt + REDACT_BLOCK / 64 - 1) / (REDACT_BLOCK / 64), REDACT_BLOCK, 0, st>>>(
-            R, text, offs, n_utt, e->fd, e->n_find, out_offs, e->span_offs, e->d_err, out, spans, e->hist);
+        if (n_chunks > 0)
+            k_redact<<<(n_chunks + REDACT_TILE_CHUNKS - 1) / REDACT_TILE_CHUNKS, REDACT_BLOCK, 0, st>>>(
+                R, text, offs, n_utt, e->first_utt, n_chunks, e->fd, e->n_find, out_offs, e->span_offs, e->d_err,
+                out, spans, e->hist);
         k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
                                                           e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
-    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(e->tev[6], st));
     return PII_OK;
 }
@@ -993,6 +1473,49 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.excl_ids = (const uint16_t*)at(i_ei);
     R.tok_off = (const uint32_t*)at(i_to);
     R.tok_bytes = (const uint8_t*)at(i_tb);
+    {   // LDS image for the pair kernels (RB_* order)
+        std::vector<std::pair<const void*, size_t>> parts(RB_N);
+        auto sec = [&](const char* nm) { return std::make_pair((const void*)find(nm)->data, (size_t)find(nm)->bytes); };
+        parts[RB_PTRANS] = sec("pool.trans");
+        parts[RB_PFLAGS] = sec("pool.flags");
+        parts[RB_PCMAP] = sec("pool.cmap");
+        parts[RB_FDESC] = sec("det.first_desc");
+        parts[RB_HDESC] = sec("hot.dfa_desc");
+        parts[RB_HRULE] = sec("hot.rule");
+        parts[RB_DTYPE] = sec("det.type");
+        parts[RB_DVAL] = sec("det.validator");
+        parts[RB_DLIK] = sec("det.lik");
+        parts[RB_DEX] = sec("det.exidx");
+        parts[RB_VEN] = sec("var.enabled");
+        parts[RB_VMIN] = sec("var.minlik");
+        parts[RB_ROFF] = sec("var.rule_off");
+        parts[RB_RIDS] = sec("var.rule_ids");
+        parts[RB_XOFF] = sec("var.excl_off");
+        parts[RB_XIDS] = sec("var.excl_ids");
+        parts[RB_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
+        parts[RB_AOFF] = sec("scan.d.acc_off");
+        parts[RB_AIDS] = sec("scan.d.acc_ids");
+        parts[RB_CMAP2] = sec("scan.cmap2");
+        size_t off = 0;
+        for (int i = 0; i < RB_N; ++i) {
+            e->ro.off[i] = (uint32_t)off;
+            off += (parts[i].second + 15) & ~(size_t)15;
+        }
+        e->ro.total = (uint32_t)off;
+        if (off > 160 * 1024) return fail("resolve tables do not fit in LDS");
+        std::vector<uint8_t> img(off, 0);
+        for (int i = 0; i < RB_N; ++i) std::memcpy(img.data() + e->ro.off[i], parts[i].first, parts[i].second);
+        if (hipMalloc(&e->d_rblob, off) != hipSuccess ||
+            hipMemcpy(e->d_rblob, img.data(), off, hipMemcpyHostToDevice) != hipSuccess)
+            return fail("resolve table upload failed");
+        if (off > 64 * 1024 &&
+            (hipFuncSetAttribute((const void*)k_pair_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)off) != hipSuccess ||
+             hipFuncSetAttribute((const void*)k_pair_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)off) != hipSuccess))
+            return fail("cannot raise LDS limit for the pair kernels");
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            e->n_cu = prop.multiProcessorCount;
+    }
     e->scan_lds = 512 + (size_t)((R.SD * R.CD + 1) / 2) * 4 + (size_t)((R.SK * R.CK + 1) / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     if (e->scan_lds > 64 * 1024 &&
@@ -1005,7 +1528,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     const size_t ns = std::max<uint32_t>(1, n_conv_slots);
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
         hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, 256 * 8) != hipSuccess ||
-        hipMalloc(&e->d_err, 16) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess)
+        hipMalloc(&e->d_err, 16) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
+        hipMalloc(&e->pair_count, 16) != hipSuccess)
         return fail("state allocation failed");
     if (hipHostMalloc(&e->h_totals, 64) != hipSuccess) return fail("pinned allocation failed");
     std::vector<int32_t> g(ns, -1);
@@ -1022,8 +1546,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
 int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->kw, e->ctx, e->agg_v, e->commit,
+    void* ptrs[] = {e->d_rules, e->d_rblob, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->pairs, e->pair_count, e->lane_pair, e->lane_np, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx};
     for (void* p : ptrs)
@@ -1085,8 +1609,20 @@ int pii_scan_redact_device(pii_engine* e, const uint8_t* d_bytes, const uint64_t
 int pii_sync(pii_engine* e, uint64_t totals[3]) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipEventSynchronize(e->tev[6]));
-    const char* names[] = {"scan", "context", "resolve", "offsets", "redact"};
-    (void)names;
+    for (int attempt = 0; (e->h_totals[2] & ERR_QUEUE) && attempt < 4; ++attempt) {
+        // the (start, pattern) pair queue overflowed: grow it to the exact need and run the batch again
+        // (the conversation context was not committed, so the re-run is idempotent)
+        const uint64_t need = e->h_totals[3] + 4096;
+        int rc = grow(e, e->pairs, need);
+        if (rc) return rc;
+        e->pair_cap = need;
+        const pii_engine::Call c = e->last;
+        e->epoch += 0;
+        rc = run_pipeline(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
+                          c.spans, c.span_cap, c.ctx_info, c.st);
+        if (rc) return rc;
+        HIPCHK(hipEventSynchronize(e->tev[6]));
+    }
     float tot = 0;
     for (int i = 0; i < 5; ++i) {
         float ms = 0;
@@ -1103,6 +1639,7 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
     const uint64_t f = e->h_totals[2];
     if (f & ERR_SLOT) return PII_E_ARG;
     if (f & ERR_ORDER) return PII_E_ORDER;
+    if (f & ERR_QUEUE) return PII_E_NOMEM;
     if (f & ERR_CAPACITY) return PII_E_CAPACITY;
     return PII_OK;
 }
