@@ -1440,7 +1440,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
            i_ro = addsec("var.rule_off"), i_ri = addsec("var.rule_ids"), i_eo = addsec("var.excl_off"),
            i_ei = addsec("var.excl_ids"), i_to = add(tok_off.data(), tok_off.size() * 4),
            i_tb = add(tok.data(), tok.size());
-    if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+    if (hipSetDevice(device) != hipSuccess) { e->err = "hipSetDevice failed"; pii_engine_destroy(e); return PII_E_DEVICE; }
     if (hipMalloc(&e->d_rules, total) != hipSuccess) return fail("hipMalloc rules failed");
     std::vector<uint8_t> host(total, 0);
     for (auto& p : puts) std::memcpy(host.data() + p.off, p.src, p.bytes);
