@@ -1,8 +1,9 @@
 // pii_device.h - per-lane building blocks of the scan-and-redact pipeline (gfx950).
 //
-// Validators restate SURVEY.md Appendix A.1 / oracle/pii_oracle.py (v_luhn ... v_iban), the DFA
-// runners execute the tables built by context-based-pii_amd/compiler.py.  Everything here is a
-// plain __device__ function; the kernels in pii_engine.hip compose them.
+// Validators restate SURVEY.md Appendix A.1 / oracle/pii_oracle.py (v_luhn ... v_iban) as forward
+// single-pass byte machines; the DFA runners execute the tables built by
+// context-based-pii_amd/compiler.py.  Text is read through 16-byte windows assembled from aligned
+// 16-byte loads (never a byte load per step, never a chunk outside the bytes asked for).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,61 +18,118 @@ __device__ __forceinline__ bool is_word(uint32_t c) {
 }
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
 
-// ---------------------------------------------------------------------------------- validators
-// SURVEY A.1 / B.4.  q = matched bytes [0, n).
-__device__ inline bool v_luhn(const uint8_t* q, int n) {
-    int s = 0, cnt = 0;
-    for (int i = n - 1; i >= 0; --i) {
-        uint32_t c = q[i];
-        if (!is_digit(c)) continue;
-        int x = (int)(c - '0');
-        if (cnt & 1) {
-            x *= 2;
-            if (x > 9) x -= 9;
-        }
-        s += x;
-        ++cnt;
+// ---------------------------------------------------------------------------------- text windows
+// 16 bytes starting at byte o (0..15) of the 32-byte window {a, b}
+__device__ __forceinline__ uint4 window16(const uint4& a, const uint4& b, uint32_t o) {
+    const uint32_t d = o >> 2, s = o & 3;
+    const uint32_t w0 = a.x, w1 = a.y, w2 = a.z, w3 = a.w, w4 = b.x, w5 = b.y, w6 = b.z, w7 = b.w;
+    const uint32_t v0 = d == 0 ? w0 : d == 1 ? w1 : d == 2 ? w2 : w3;
+    const uint32_t v1 = d == 0 ? w1 : d == 1 ? w2 : d == 2 ? w3 : w4;
+    const uint32_t v2 = d == 0 ? w2 : d == 1 ? w3 : d == 2 ? w4 : w5;
+    const uint32_t v3 = d == 0 ? w3 : d == 1 ? w4 : d == 2 ? w5 : w6;
+    const uint32_t v4 = d == 0 ? w4 : d == 1 ? w5 : d == 2 ? w6 : w7;
+    return make_uint4(__builtin_amdgcn_alignbyte(v1, v0, s), __builtin_amdgcn_alignbyte(v2, v1, s),
+                      __builtin_amdgcn_alignbyte(v3, v2, s), __builtin_amdgcn_alignbyte(v4, v3, s));
+}
+
+// bytes [src, src + 16) as a uint4, reading only the aligned 16-byte chunks that hold a byte of
+// [src + need_lo, src + need_hi) (so never a chunk outside the caller's buffer); other bytes are 0
+__device__ __forceinline__ uint4 load16(const uint8_t* src, int need_lo, int need_hi) {
+    const uintptr_t a = (uintptr_t)src & ~(uintptr_t)15;
+    const uint4* p = reinterpret_cast<const uint4*>(a);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 x = a + 16 > (uintptr_t)(src + need_lo) ? p[0] : z;
+    const uint4 y = a + 16 < (uintptr_t)(src + need_hi) ? p[1] : z;
+    return window16(x, y, (uint32_t)((uintptr_t)src - a));
+}
+
+__device__ __forceinline__ uint32_t bytemask(int n) {   // low n bytes (n clamped to [0, 4])
+    return n <= 0 ? 0u : (n >= 4 ? 0xffffffffu : (1u << (8 * n)) - 1u);
+}
+
+// shift a 16-byte window right by one byte
+__device__ __forceinline__ void shr8(uint4& w) {
+    w.x = __builtin_amdgcn_alignbyte(w.y, w.x, 1);
+    w.y = __builtin_amdgcn_alignbyte(w.z, w.y, 1);
+    w.z = __builtin_amdgcn_alignbyte(w.w, w.z, 1);
+    w.w >>= 8;
+}
+
+// Iterate the bytes of text[lo, hi) in order: BODY sees `c` (the byte) and `i` (its index relative
+// to lo).  One window load per 16 bytes, a runtime loop per byte (a wavefront leaves it as soon as
+// its last lane is done, instead of stepping through whole predicated chunks).
+#define PII_FOR_BYTES(text, lo, hi, ...)                                                         \
+    for (int _j = (lo); _j < (hi); _j += 16) {                                                    \
+        const int _n = (hi) - _j < 16 ? (hi) - _j : 16;                                           \
+        uint4 _w = load16((text) + _j, 0, _n);                                                    \
+        for (int _k = 0; _k < _n; ++_k) {                                                         \
+            const uint32_t c = _w.x & 0xffu;                                                      \
+            const int i = _j - (lo) + _k;                                                         \
+            (void)i;                                                                              \
+            __VA_ARGS__;                                                                          \
+            shr8(_w);                                                                             \
+        }                                                                                         \
     }
+
+// ---------------------------------------------------------------------------------- validators
+// SURVEY A.1 / B.4, one forward pass over q[0, n).
+__device__ inline bool v_luhn(const uint8_t* q, int n) {
+    // digit k (from the left) is doubled iff (cnt - 1 - k) is odd: keep both parities' sums
+    int sa = 0, sb = 0, cnt = 0;
+    PII_FOR_BYTES(q, 0, n, {
+        if (is_digit(c)) {
+            const int d = (int)(c - '0');
+            const int dd = d * 2 > 9 ? d * 2 - 9 : d * 2;
+            if (cnt & 1) {
+                sa += dd;
+                sb += d;
+            } else {
+                sa += d;
+                sb += dd;
+            }
+            ++cnt;
+        }
+    })
+    const int s = ((cnt - 1) & 1) ? sb : sa;
     return cnt >= 2 && s % 10 == 0;
 }
 
-// digit-field validators accumulate the fields on the fly (no local arrays -> no scratch)
 __device__ inline bool v_nanp(const uint8_t* q, int n) {
     int k = 0;
     bool ok = true;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t c = q[i];
-        if (!is_digit(c)) continue;
-        if ((k == 0 || k == 3) && c < '2') ok = false;
-        ++k;
-    }
+    PII_FOR_BYTES(q, 0, n, {
+        if (is_digit(c)) {
+            if ((k == 0 || k == 3) && c < '2') ok = false;
+            ++k;
+        }
+    })
     return ok && k == 10;
 }
 
 __device__ inline bool v_ssn(const uint8_t* q, int n) {
     int k = 0;
     uint32_t area = 0, group = 0, serial = 0;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t c = q[i];
-        if (!is_digit(c)) continue;
-        const uint32_t d = c - '0';
-        if (k < 3) area = area * 10 + d;
-        else if (k < 5) group = group * 10 + d;
-        else serial = serial * 10 + d;
-        ++k;
-    }
+    PII_FOR_BYTES(q, 0, n, {
+        if (is_digit(c)) {
+            const uint32_t d = c - '0';
+            if (k < 3) area = area * 10 + d;
+            else if (k < 5) group = group * 10 + d;
+            else serial = serial * 10 + d;
+            ++k;
+        }
+    })
     return k == 9 && area != 0 && area != 666 && area < 900 && group != 0 && serial != 0;
 }
 
 __device__ inline bool v_ein(const uint8_t* q, int n) {
     int k = 0;
     uint32_t p = 0;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t c = q[i];
-        if (!is_digit(c)) continue;
-        if (k < 2) p = p * 10 + (c - '0');
-        ++k;
-    }
+    PII_FOR_BYTES(q, 0, n, {
+        if (is_digit(c)) {
+            if (k < 2) p = p * 10 + (c - '0');
+            ++k;
+        }
+    })
     if (k != 9) return false;
     const uint64_t lo = 0xfffdffffcff1fc7eull, hi = 0x0000000cfdff3f9full;   // oracle EIN_PREFIXES
     return p < 64 ? ((lo >> p) & 1) : ((hi >> (p - 64)) & 1);
@@ -80,10 +138,10 @@ __device__ inline bool v_ein(const uint8_t* q, int n) {
 __device__ inline bool v_ipv4(const uint8_t* q, int n) {
     int parts = 0, len = 0;
     uint32_t val = 0;
-    for (int i = 0; i <= n; ++i) {
-        uint32_t c = i < n ? q[i] : '.';
+    bool ok = true;
+    PII_FOR_BYTES(q, 0, n, {
         if (c == '.') {
-            if (len == 0 || len > 3 || val > 255) return false;
+            if (len == 0 || len > 3 || val > 255) ok = false;
             ++parts;
             len = 0;
             val = 0;
@@ -91,10 +149,11 @@ __device__ inline bool v_ipv4(const uint8_t* q, int n) {
             val = val * 10 + (c - '0');
             ++len;
         } else {
-            return false;
+            ok = false;
         }
-    }
-    return parts == 4;
+    })
+    if (len == 0 || len > 3 || val > 255) ok = false;     // the final field
+    return ok && parts + 1 == 4;
 }
 
 // ISO 3166-1 alpha-2, bit (a-'A')*26 + (b-'A')  (oracle ISO3166)
@@ -104,34 +163,45 @@ __constant__ const uint32_t ISO3166_BITS[22] = {0xeedf5978u, 0xdeddbdefu, 0x1584
                               0x00004002u, 0x00100000u, 0x00400408u, 0x00000001u};
 
 __device__ inline bool v_swift(const uint8_t* q, int n) {
-    const uint32_t* iso = ISO3166_BITS;
     if (n != 8 && n != 11) return false;
-    uint32_t a = q[4] - 'A', b = q[5] - 'A';
+    const uint4 w = load16(q, 4, 6);
+    const uint32_t a = ((w.y >> 0) & 0xffu) - 'A', b = ((w.y >> 8) & 0xffu) - 'A';
     if (a >= 26u || b >= 26u) return false;
-    uint32_t i = a * 26 + b;
-    return (iso[i >> 5] >> (i & 31)) & 1;
+    const uint32_t i = a * 26 + b;
+    return (ISO3166_BITS[i >> 5] >> (i & 31)) & 1;
 }
 
+// mod-97 of the string rotated by four characters (spaces skipped), in one forward pass:
+// value(chars[4:]) * 10^digits(chars[0:4]) + value(chars[0:4])  (mod 97)
 __device__ inline bool v_iban(const uint8_t* q, int n) {
     int len = 0;
-    for (int i = 0; i < n; ++i) len += q[i] != ' ';
-    if (len < 15 || len > 34) return false;
-    // rotate: chars 4.. then 0..3 (spaces skipped)
-    uint32_t r = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        int k = 0;
-        for (int i = 0; i < n; ++i) {
-            uint32_t c = q[i];
-            if (c == ' ') continue;
-            bool take = pass == 0 ? k >= 4 : k < 4;
-            ++k;
-            if (!take) continue;
-            if (is_digit(c)) r = (r * 10 + (c - '0')) % 97;
-            else if (c - 'A' < 26u) r = (r * 100 + (c - 55)) % 97;
-            else return false;
+    uint32_t head = 0, headpow = 1, tail = 0;
+    bool ok = true;
+    PII_FOR_BYTES(q, 0, n, {
+        if (c != ' ') {
+            uint32_t v, m;
+            if (is_digit(c)) {
+                v = c - '0';
+                m = 10;
+            } else if (c - 'A' < 26u) {
+                v = c - 55;
+                m = 100;
+            } else {
+                ok = false;
+                v = 0;
+                m = 1;
+            }
+            if (len < 4) {
+                head = (head * m + v) % 97;
+                headpow = (headpow * m) % 97;
+            } else {
+                tail = (tail * m + v) % 97;
+            }
+            ++len;
         }
-    }
-    return r == 1;
+    })
+    if (!ok || len < 15 || len > 34) return false;
+    return (tail * headpow + head) % 97 == 1;
 }
 
 __device__ inline bool validate(int id, const uint8_t* q, int n) {
@@ -150,86 +220,53 @@ __device__ inline bool validate(int id, const uint8_t* q, int n) {
 
 // ---------------------------------------------------------------------------------- DFA runners
 // descriptor layout (compiler.put): tr_off, fl_off, cm_off, ncols, start_bot, start_w, start_n, n_states
+// In the kernels' LDS images every transition entry is  next_state | flags(next_state) << 14
+// (FIRST: bit 14 = a match ended before the byte just consumed, bit 15 = terminal; HOT: bit 14 =
+// accept), so one step is two dependent LDS reads (byte class, transition).
+constexpr uint32_t DFA_STATE_MASK = 0x3fffu;
 struct Pool {
     const uint16_t* trans;
-    const uint8_t* flags;
     const uint8_t* cmap;
 };
 
-template <int K>
-__device__ __forceinline__ uint32_t chunk_byte(const uint4& w) {
-    const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
-    return (x >> ((K & 3) * 8)) & 0xffu;
-}
-
-// Text access for the DFA runners: aligned 16-byte chunks (one chunk prefetched ahead) with
-// compile-time byte extraction, instead of one dependent byte load per DFA step.  A chunk is only
-// loaded when it contains at least one byte of the requested range; an aligned 16-byte block never
-// straddles a page, so reading all of it is safe.
-#define PII_DFA_STREAM(BODY)                                                                      \
-    {                                                                                             \
-        const uint8_t* pa = text + lo;                                                            \
-        const uint4* cp = reinterpret_cast<const uint4*>((uintptr_t)pa & ~(uintptr_t)15);         \
-        int j = lo - (int)((uintptr_t)pa & 15);   /* position of byte 0 of chunk *cp */           \
-        uint4 w = *cp;                                                                            \
-        uint4 wn = j + 16 < hi ? cp[1] : w;                                                       \
-        for (;;) {                                                                                \
-            const uint4 cur = w;                                                                  \
-            w = wn;                                                                               \
-            if (j + 32 < hi) wn = cp[2];                                                          \
-            BODY(0) BODY(1) BODY(2) BODY(3) BODY(4) BODY(5) BODY(6) BODY(7)                       \
-            BODY(8) BODY(9) BODY(10) BODY(11) BODY(12) BODY(13) BODY(14) BODY(15)                 \
-            j += 16;                                                                              \
-            ++cp;                                                                                 \
-            if (j >= hi) break;                                                                   \
-        }                                                                                         \
-    }
-
 // Anchored leftmost-first run of FIRST DFA `d` from byte s of text[0, L): returns the end `re`
-// would report for a match starting at s, or -1.  (compiler.build_first_dfa: flags bit0 = a match
-// ended before the char just consumed, bit1 = terminal.)
+// would report for a match starting at s, or -1.  (compiler.build_first_dfa semantics.)
 __device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L) {
     const uint16_t* tr = pool.trans + d[0];
-    const uint8_t* fl = pool.flags + d[1];
     const uint8_t* cm = pool.cmap + d[2];
-    const int nc = d[3];
-    int st = s == 0 ? d[4] : (is_word(text[s - 1]) ? d[5] : d[6]);
+    const uint32_t nc = (uint32_t)d[3];
+    // the start state depends on the kind of text[s-1]: read it as the run's first window byte
+    constexpr uint32_t UNSET = 0xffffffffu;
+    uint32_t st = s == 0 ? (uint32_t)d[4] : UNSET;
+    const int lo = s == 0 ? 0 : s - 1;
     int last = -1;
-    if (s < L) {
-        const int lo = s, hi = L;
-#define PII_FIRST_STEP(K)                                                                         \
-        if (j + (K) >= lo && j + (K) < hi) {                                                      \
-            st = tr[st * nc + cm[chunk_byte<K>(cur)]];                                            \
-            const uint32_t f = fl[st];                                                            \
-            if (f & 1) last = j + (K);                                                            \
-            if (f & 2) return last;                                                               \
+    PII_FOR_BYTES(text, lo, L, {
+        if (st == UNSET) {
+            st = (uint32_t)(is_word(c) ? d[5] : d[6]);
+        } else {
+            const uint32_t e = tr[st * nc + cm[c]];
+            st = e & DFA_STATE_MASK;
+            if (e & 0x4000u) last = lo + i;
+            if (e & 0x8000u) return last;
         }
-        PII_DFA_STREAM(PII_FIRST_STEP)
-#undef PII_FIRST_STEP
-    }
-    st = tr[st * nc + nc - 1];
-    if (fl[st] & 1) last = L;
+    })
+    if (st == UNSET) st = (uint32_t)(is_word(text[lo]) ? d[5] : d[6]);     // s == L
+    if (tr[st * nc + nc - 1] & 0x4000u) last = L;
     return last;
 }
 
 // Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics)
 __device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
     const uint16_t* tr = pool.trans + d[0];
-    const uint8_t* fl = pool.flags + d[1];
     const uint8_t* cm = pool.cmap + d[2];
-    const int nc = d[3];
-    int st = d[4];
-    if (lo < hi) {
-#define PII_HOT_STEP(K)                                                                           \
-        if (j + (K) >= lo && j + (K) < hi) {                                                      \
-            st = tr[st * nc + cm[chunk_byte<K>(cur)]];                                            \
-            if (fl[st]) return true;                                                              \
-        }
-        PII_DFA_STREAM(PII_HOT_STEP)
-#undef PII_HOT_STEP
-    }
-    st = tr[st * nc + nc - 1];
-    return fl[st] != 0;
+    const uint32_t nc = (uint32_t)d[3];
+    uint32_t st = (uint32_t)d[4];
+    PII_FOR_BYTES(text, lo, hi, {
+        const uint32_t e = tr[st * nc + cm[c]];
+        if (e & 0x4000u) return true;
+        st = e & DFA_STATE_MASK;
+    })
+    return (tr[st * nc + nc - 1] & 0x4000u) != 0;
 }
 
 }  // namespace pii

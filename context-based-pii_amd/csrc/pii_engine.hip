@@ -47,9 +47,9 @@ constexpr int KW_NONE = 0x7fff;
 enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8 };
 
 struct Event {
-    uint32_t pos;   // candidate start, relative to the utterance
-    uint16_t sd;    // D automaton row (state * CD) BEFORE the reporting transition
-    uint16_t sk;    // K automaton row before it
+    uint32_t pos;   // candidate start, relative to the batch base
+    uint16_t sd;    // D transition index (row + class) that reported it
+    uint16_t sk;    // K transition index (row + class)
 };
 
 struct RulesDev {
@@ -70,7 +70,6 @@ struct RulesDev {
     const int32_t* first_desc;  // [P*8]
     const int32_t* hot_rule;    // [n_hot*4] wb, wa, fixed, rel
     const int32_t* hot_desc;    // [n_hot*8]
-    Pool pool;
     const uint8_t* var_enabled;  // [V*T]
     const uint8_t* var_minlik;   // [V]
     const uint32_t* rule_off;    // [V*T+1]
@@ -160,8 +159,8 @@ __device__ __forceinline__ void scan_bot(const RulesDev& R, const uint16_t* s_td
     if ((nd | nk) & 0x8000u) {
         Event e;
         e.pos = pos;
-        e.sd = (uint16_t)sd;
-        e.sk = (uint16_t)sk;
+        e.sd = (uint16_t)(sd + (uint32_t)(R.CD - 1));
+        e.sk = (uint16_t)(sk + (uint32_t)(R.CK - 1));
         evl[cnt++] = e;
     }
     sd = (uint32_t)R.d_start;
@@ -177,8 +176,8 @@ __device__ __forceinline__ void scan_bot(const RulesDev& R, const uint16_t* s_td
             if (__builtin_expect(((nd | nk) & 0x8000u) != 0, 0)) {                                \
                 Event e;                                                                          \
                 e.pos = (uint32_t)(jj + 1 - base);                                                \
-                e.sd = (uint16_t)sd;                                                              \
-                e.sk = (uint16_t)sk;                                                              \
+                e.sd = (uint16_t)(sd + (cc[K] & 0xffu));                                          \
+                e.sk = (uint16_t)(sk + (cc[K] >> 8));                                             \
                 evl[cnt++] = e;                                                                   \
             }                                                                                     \
             sd = nd & 0x7fffu;                                                                    \
@@ -412,28 +411,43 @@ __global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int16_t* _
 //   k_pair_first per pair: anchored leftmost-first run -> end (or -1)      [lockstep DFA runs]
 //   k_pair_eval  per matched pair: validator + hotword windows of the row's context variant -> likelihood
 //   k_select     per scan lane: finditer skipping, exclusion, overlap resolution -> kept findings
-struct Pair {
-    uint32_t u;     // utterance
-    uint32_t s;     // start, relative to the utterance
-    uint16_t p;     // detector pattern
-    int16_t lik;    // likelihood after validation + hotwords; -1 = invalid
-    int32_t e;      // leftmost-first end, -1 = no match
+struct PairLoc {       // where a candidate is (16 B: one dwordx4)
+    uint32_t u;        // utterance
+    uint32_t s;        // candidate start, relative to the batch base
+    uint32_t ustart;   // utterance start, relative to the batch base
+    uint32_t uend;     // utterance end, relative to the batch base
 };
-enum RB {
-    RB_PTRANS, RB_PFLAGS, RB_PCMAP, RB_FDESC, RB_HDESC, RB_HRULE, RB_DTYPE, RB_DVAL, RB_DLIK, RB_DEX,
-    RB_VEN, RB_VMIN, RB_ROFF, RB_RIDS, RB_XOFF, RB_XIDS, RB_TOKOFF, RB_AOFF, RB_AIDS, RB_CMAP2, RB_N
-};
-struct RBOffs {
-    uint32_t off[RB_N];
-    uint32_t total;   // bytes, multiple of 16
+struct PairRes {       // what it turned into (8 B)
+    uint16_t p;        // detector pattern
+    int16_t lik;       // likelihood after validation + hotwords; -1 = invalid
+    int32_t e;         // leftmost-first match end, relative to the utterance start; -1 = no match
 };
 
-__global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint8_t* __restrict__ text,
-                                               const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
-                                               uint32_t n_chunks, const Event* __restrict__ ev,
-                                               const uint32_t* __restrict__ lane_cnt, const uint8_t* __restrict__ role,
-                                               int16_t* __restrict__ kw, Pair* __restrict__ pairs, uint64_t pair_cap,
-                                               unsigned long long* __restrict__ pair_count,
+// LDS images of rule tables, one per kernel (only what that kernel reads, so the pair kernels keep
+// two 1024-thread workgroups per CU).  Sections are 16-byte aligned; off[] are byte offsets.
+constexpr int IMG_MAX = 12;
+struct LdsImage {
+    uint32_t off[IMG_MAX];
+    uint32_t total;    // bytes, multiple of 16
+};
+enum { FI_TRANS, FI_CMAP, FI_DESC, FI_N };
+enum { EV_TRANS, EV_CMAP, EV_HDESC, EV_HRULE, EV_DTYPE, EV_DVAL, EV_DLIK, EV_ROFF, EV_RIDS, EV_N };
+enum { SE_DTYPE, SE_VEN, SE_VMIN, SE_DEX, SE_XOFF, SE_XIDS, SE_TOKOFF, SE_N };
+
+constexpr int PAIR_BLOCK = 1024;
+
+// pair-queue segment of workgroup g in k_pair_first / k_pair_eval: [g*seg, (g+1)*seg)
+__device__ __forceinline__ uint64_t pair_segment(uint64_t n, uint32_t nseg) {
+    const uint64_t per = (n + nseg - 1) / nseg;
+    return (per + PAIR_BLOCK - 1) / PAIR_BLOCK * PAIR_BLOCK;
+}
+
+__global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint64_t* __restrict__ offs,
+                                               const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+                                               const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
+                                               const uint8_t* __restrict__ role, int16_t* __restrict__ kw,
+                                               PairLoc* __restrict__ ploc, PairRes* __restrict__ pres,
+                                               uint64_t pair_cap, unsigned long long* __restrict__ pair_count,
                                                uint64_t* __restrict__ lane_pair, uint32_t* __restrict__ lane_np,
                                                uint32_t* __restrict__ err) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -448,7 +462,7 @@ __global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint8_t* 
         evl = ev + ((int64_t)offs[u0] - base);
         u_top = (int64_t)first_utt[c + 1] - 1;
     }
-    // pass 1: count pairs, keyword groups
+    // pass 1: count pairs, keyword groups of AGENT rows
     uint32_t np = 0;
     {
         int64_t u = u_top;
@@ -465,13 +479,10 @@ __global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint8_t* 
                 s_u = (int64_t)offs[u] - base;
                 agent = role[u] == PII_ROLE_AGENT;
             }
-            const uint32_t cc = pos == s_u ? 0xffffffffu : (uint32_t)R.cmap2[text[base + pos - 1]];
-            const uint32_t cd = pos == s_u ? (uint32_t)(R.CD - 1) : (cc & 0xffu);
-            const uint32_t acc = R.d_accid[E.sd + cd];
+            const uint32_t acc = R.d_accid[E.sd];
             np += R.d_acc_off[acc + 1] - R.d_acc_off[acc];
             if (agent) {
-                const uint32_t ck = pos == s_u ? (uint32_t)(R.CK - 1) : (cc >> 8);
-                const uint32_t a = R.k_accid[E.sk + ck];
+                const uint32_t a = R.k_accid[E.sk];
                 if (a) g = min(g, (int)R.k_acc_min[a]);
             }
         }
@@ -500,242 +511,363 @@ __global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint8_t* 
     uint64_t w = my + np;
     int64_t u = u_top;
     int64_t s_u = (int64_t)offs[u] - base;
+    int64_t e_u = (int64_t)offs[u + 1] - base;
     for (uint32_t k = 0; k < cnt; ++k) {
         const Event E = evl[k];
         const int64_t pos = E.pos;
         while (pos < s_u) {
             --u;
+            e_u = s_u;
             s_u = (int64_t)offs[u] - base;
         }
-        const uint32_t cd = pos == s_u ? (uint32_t)(R.CD - 1) : (uint32_t)(R.cmap2[text[base + pos - 1]] & 0xffu);
-        const uint32_t acc = R.d_accid[E.sd + cd];
+        const uint32_t acc = R.d_accid[E.sd];
         const uint32_t a0 = R.d_acc_off[acc], a1 = R.d_acc_off[acc + 1];
         w -= a1 - a0;
+        PairLoc Lc;
+        Lc.u = (uint32_t)u;
+        Lc.s = (uint32_t)pos;
+        Lc.ustart = (uint32_t)s_u;
+        Lc.uend = (uint32_t)e_u;
         for (uint32_t i = a0; i < a1; ++i) {
-            Pair P;
-            P.u = (uint32_t)u;
-            P.s = (uint32_t)(pos - s_u);
+            PairRes P;
             P.p = R.d_acc_ids[i];
             P.lik = -1;
             P.e = -1;
-            pairs[w + (i - a0)] = P;
+            ploc[w + (i - a0)] = Lc;
+            pres[w + (i - a0)] = P;
         }
     }
 }
 
-__device__ __forceinline__ const uint8_t* load_rblob(const uint4* __restrict__ rblob, const RBOffs& ro, uint4* lds4) {
-    for (uint32_t i = threadIdx.x; i < ro.total / 16; i += blockDim.x) lds4[i] = rblob[i];
+__device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ img, uint32_t total, uint4* lds4) {
+    for (uint32_t i = threadIdx.x; i < total / 16; i += blockDim.x) lds4[i] = img[i];
     __syncthreads();
     return reinterpret_cast<const uint8_t*>(lds4);
 }
 
-__global__ __launch_bounds__(1024) void k_pair_first(const uint4* __restrict__ rblob, const RBOffs ro,
-                                                     const uint8_t* __restrict__ text,
-                                                     const uint64_t* __restrict__ offs,
-                                                     const unsigned long long* __restrict__ pair_count,
-                                                     uint64_t pair_cap, Pair* __restrict__ pairs) {
+// per pair: anchored leftmost-first run.  Workgroup g owns one contiguous segment of the queue and
+// compacts its matched pairs, in queue order, into the same segment of `matched` (no global atomics).
+__global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
+                                                           const uint8_t* __restrict__ text0,
+                                                           const uint64_t* __restrict__ offs,
+                                                           const unsigned long long* __restrict__ pair_count,
+                                                           uint64_t pair_cap, const PairLoc* __restrict__ ploc,
+                                                           PairRes* __restrict__ pres, uint32_t* __restrict__ matched,
+                                                           uint32_t* __restrict__ mcount) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    const uint8_t* lb = load_rblob(rblob, ro, lds4);
-    const Pool pool{reinterpret_cast<const uint16_t*>(lb + ro.off[RB_PTRANS]), lb + ro.off[RB_PFLAGS],
-                    lb + ro.off[RB_PCMAP]};
-    const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + ro.off[RB_FDESC]);
+    __shared__ uint32_t s_wcnt[PAIR_BLOCK / 64];
+    __shared__ uint32_t s_bucket[P_MAX], s_bstart[P_MAX];
+    __shared__ uint16_t s_perm[PAIR_BLOCK];
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[FI_TRANS]), lb + li.off[FI_CMAP]};
+    const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + li.off[FI_DESC]);
     const uint64_t n = min((uint64_t)*pair_count, pair_cap);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        Pair P = pairs[i];
-        const uint64_t sa = offs[P.u];
-        const int L = (int)(offs[P.u + 1] - sa);
-        P.e = first_run(pool, fdesc + 8 * P.p, text + sa, (int)P.s, L);
-        pairs[i].e = P.e;
+    const uint8_t* text = text0 + offs[0];     // pair positions are relative to the batch base
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t seg = pair_segment(n, gridDim.x);
+    const uint64_t lo = blockIdx.x * seg, hi = min(n, lo + seg);
+    uint32_t cnt = 0;
+    for (uint64_t b = lo; b < hi; b += PAIR_BLOCK) {       // uniform trip count in the workgroup
+        // counting sort of the batch by pattern, so a wavefront runs one automaton on runs of
+        // similar length (its step count is the longest run among its lanes)
+        if (threadIdx.x < P_MAX) s_bucket[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t i0 = b + threadIdx.x;
+        uint32_t p0 = 0, rank = 0;
+        if (i0 < hi) {
+            p0 = pres[i0].p;
+            rank = atomicAdd(&s_bucket[p0], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {                               // exclusive scan of the P_MAX buckets
+            const uint32_t v = s_bucket[threadIdx.x];
+            uint32_t inc = v;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d);
+                if (lane >= d) inc += o;
+            }
+            s_bstart[threadIdx.x] = inc - v;
+        }
+        __syncthreads();
+        if (i0 < hi) s_perm[s_bstart[p0] + rank] = (uint16_t)threadIdx.x;
+        __syncthreads();
+        const uint32_t nb = (uint32_t)min((uint64_t)PAIR_BLOCK, hi - b);
+        const uint64_t i = b + ((uint32_t)threadIdx.x < nb ? s_perm[threadIdx.x] : 0u);
+        int e = -1;
+        if ((uint32_t)threadIdx.x < nb) {
+            const PairLoc L = ploc[i];
+            const int p = pres[i].p;
+            const uint8_t* t0 = text + L.ustart;
+            e = first_run(pool, fdesc + 8 * p, t0, (int)(L.s - L.ustart), (int)(L.uend - L.ustart));
+            if (e >= 0) pres[i].e = e;
+        }
+        const uint64_t m = __ballot(e >= 0);
+        if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < PAIR_BLOCK / 64; ++w) {
+            const uint32_t c = s_wcnt[w];
+            before += w < wave ? c : 0u;
+            total += c;
+        }
+        if (e >= 0) matched[lo + cnt + before + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)i;
+        cnt += total;
     }
+    if (threadIdx.x == 0) mcount[blockIdx.x] = cnt;
 }
 
-__global__ __launch_bounds__(1024) void k_pair_eval(const RulesDev R, const uint4* __restrict__ rblob, const RBOffs ro,
-                                                    const uint8_t* __restrict__ text,
-                                                    const uint64_t* __restrict__ offs,
-                                                    const uint8_t* __restrict__ role, const int16_t* __restrict__ ctx,
-                                                    const unsigned long long* __restrict__ pair_count,
-                                                    uint64_t pair_cap, Pair* __restrict__ pairs) {
+// per matched pair: validator + hotword windows of the row's context variant -> likelihood
+__global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
+                                                          const uint8_t* __restrict__ text0,
+                                                          const uint64_t* __restrict__ offs,
+                                                          const uint8_t* __restrict__ role,
+                                                          const int16_t* __restrict__ ctx,
+                                                          const unsigned long long* __restrict__ pair_count,
+                                                          uint64_t pair_cap, const uint32_t* __restrict__ matched,
+                                                          const uint32_t* __restrict__ mcount, uint32_t nseg,
+                                                          const PairLoc* __restrict__ ploc,
+                                                          PairRes* __restrict__ pres) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    const uint8_t* lb = load_rblob(rblob, ro, lds4);
-    const Pool pool{reinterpret_cast<const uint16_t*>(lb + ro.off[RB_PTRANS]), lb + ro.off[RB_PFLAGS],
-                    lb + ro.off[RB_PCMAP]};
-    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + ro.off[RB_HDESC]);
-    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + ro.off[RB_HRULE]);
-    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + ro.off[RB_DTYPE]);
-    const uint8_t* dval = lb + ro.off[RB_DVAL];
-    const uint8_t* dlik = lb + ro.off[RB_DLIK];
-    const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + ro.off[RB_ROFF]);
-    const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + ro.off[RB_RIDS]);
-    const int T = R.T;
-    const uint64_t n = min((uint64_t)*pair_count, pair_cap);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const Pair P = pairs[i];
-        if (P.e < 0) continue;
-        const uint64_t sa = offs[P.u];
-        const int L = (int)(offs[P.u + 1] - sa);
-        const uint8_t* t0 = text + sa;
-        const int s = (int)P.s, e = P.e;
-        int lik = -1;
-        if (validate(dval[P.p], t0 + s, e - s)) {
-            const int v = (role[P.u] == PII_ROLE_CUSTOMER && ctx[P.u] >= 0) ? ctx[P.u] + 1 : 0;
-            const int t = dtype[P.p];
-            lik = dlik[P.p];
-            const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
-            for (uint32_t q = r0; q < r1; ++q) {
-                const int h = rids[q];
-                const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
-                const int fixed = hrule[4 * h + 2], rel = hrule[4 * h + 3];
-                bool hit = false;
-                if (wb > 0) hit = hot_run(pool, hdesc + 8 * h, t0, s - wb > 0 ? s - wb : 0, s);
-                if (!hit && wa > 0) hit = hot_run(pool, hdesc + 8 * h, t0, e, e + wa < L ? e + wa : L);
-                if (hit) {
-                    if (fixed) {
-                        lik = fixed;
-                    } else {
-                        lik += rel;
-                        lik = lik < 1 ? 1 : (lik > 5 ? 5 : lik);
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
+    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
+    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[EV_DTYPE]);
+    const uint8_t* dval = lb + li.off[EV_DVAL];
+    const uint8_t* dlik = lb + li.off[EV_DLIK];
+    const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + li.off[EV_ROFF]);
+    const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + li.off[EV_RIDS]);
+    const uint8_t* text = text0 + offs[0];
+    const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg);
+    for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
+        const uint32_t m = mcount[g];
+        const uint32_t* ms = matched + (uint64_t)g * seg;
+        for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) {
+            const uint32_t i = ms[k];
+            const PairLoc Lc = ploc[i];
+            const PairRes P = pres[i];
+            const uint8_t* t0 = text + Lc.ustart;
+            const int L = (int)(Lc.uend - Lc.ustart);
+            const int s = (int)(Lc.s - Lc.ustart), e = P.e;
+            int lik = -1;
+            if (validate(dval[P.p], t0 + s, e - s)) {
+                const uint32_t u = Lc.u;
+                const int v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
+                const int t = dtype[P.p];
+                lik = dlik[P.p];
+                const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
+                for (uint32_t q = r0; q < r1; ++q) {
+                    const int h = rids[q];
+                    const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
+                    const int fixed = hrule[4 * h + 2], rel = hrule[4 * h + 3];
+                    bool hit = false;
+                    if (wb > 0) hit = hot_run(pool, hdesc + 8 * h, t0, s - wb > 0 ? s - wb : 0, s);
+                    if (!hit && wa > 0) hit = hot_run(pool, hdesc + 8 * h, t0, e, e + wa < L ? e + wa : L);
+                    if (hit) {
+                        if (fixed) {
+                            lik = fixed;
+                        } else {
+                            lik += rel;
+                            lik = lik < 1 ? 1 : (lik > 5 ? 5 : lik);
+                        }
                     }
                 }
             }
+            pres[i].lik = (int16_t)lik;
         }
-        pairs[i].lik = (int16_t)lik;
     }
 }
 
 constexpr int LIVE = 8;            // register-resident "previous match end" slots per lane
 
-__global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint64_t* __restrict__ offs,
+// Per scan lane: its pairs in (utterance, start, accept-set) order.  Unmatched pairs change no state
+// (finditer skipping, exclusion and overlap only see matches), so only matched ones are decoded.
+__global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
-                                                const uint32_t* __restrict__ lane_np, const Pair* __restrict__ pairs,
+                                                const uint32_t* __restrict__ lane_np,
+                                                const PairLoc* __restrict__ ploc, const PairRes* __restrict__ pres,
                                                 uint64_t pair_cap, const uint8_t* __restrict__ role,
                                                 const int16_t* __restrict__ ctx, pii_span* __restrict__ fd,
                                                 uint32_t* __restrict__ n_find, uint32_t* __restrict__ out_len) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[SE_DTYPE]);
+    const uint8_t* ven = lb + li.off[SE_VEN];
+    const uint8_t* vmin = lb + li.off[SE_VMIN];
+    const uint8_t* dex = lb + li.off[SE_DEX];
+    const uint32_t* xoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_XOFF]);
+    const uint16_t* xids = reinterpret_cast<const uint16_t*>(lb + li.off[SE_XIDS]);
+    const uint32_t* tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_TOKOFF]);
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     const uint32_t np = lane_np[c];
     if (np == 0 || lane_pair[c] + np > pair_cap) return;     // overflowed queue: the batch is re-run
-    const Pair* pl = pairs + lane_pair[c];
-    const int64_t base = (int64_t)offs[0];
+    const PairRes* rl = pres + lane_pair[c];
+    const PairLoc* ll = ploc + lane_pair[c];
     const int T = R.T;
-    uint32_t i = 0;
-    while (i < np) {
-        const uint32_t u = pl[i].u;
-        const int64_t s_abs = (int64_t)offs[u];
-        const int L = (int)((int64_t)offs[u + 1] - s_abs);
-        const int v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
-        const int minlik = R.var_minlik[v];
-        pii_span* fdu = fd + (s_abs - base) / R.min_len;
-        int lp[LIVE], le[LIVE];
+    // per-utterance state
+    uint32_t u = 0xffffffffu;
+    int v = 0, minlik = 0, L = 0;
+    pii_span* fdu = nullptr;
+    int lp[LIVE], le[LIVE];
+    uint32_t cur_s[P_MAX];     // spill array: touched only when LIVE slots overflow
+    bool spilled = false;
+    int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
+    uint32_t ex_valid = 0;
+    int max_end = 0;
+    uint32_t nf = 0;
+    int delta = 0;
+    // per-start state
+    int s = -1, best_e = -1, best_t = 0, best_lik = 0;
 #pragma unroll
-        for (int q = 0; q < LIVE; ++q) {
-            lp[q] = -1;
-            le[q] = -1;
+    for (int q = 0; q < LIVE; ++q) {
+        lp[q] = -1;
+        le[q] = -1;
+    }
+    auto flush_start = [&]() {
+        if (best_e >= 0 && s >= max_end) {
+            pii_span f;
+            f.utt = u;
+            f.start = (uint32_t)s;
+            f.end = (uint32_t)best_e;
+            f.info_type = (uint16_t)best_t;
+            f.likelihood = (uint8_t)best_lik;
+            f.flags = 0;
+            fdu[nf++] = f;
+            max_end = best_e;
+            delta += (int)(tokoff[best_t + 1] - tokoff[best_t]) - (best_e - s);
         }
-        uint32_t cur_s[P_MAX];     // spill array: touched only when LIVE slots overflow
-        bool spilled = false;
-        int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
-        uint32_t ex_valid = 0;
-        int max_end = 0;
-        uint32_t nf = 0;
-        int64_t out = L;
-        while (i < np && pl[i].u == u) {
-            const int s = (int)pl[i].s;
-            int best_e = -1, best_t = 0, best_lik = 0;
-            for (; i < np && pl[i].u == u && (int)pl[i].s == s; ++i) {
-                const Pair P = pl[i];
-                const int p = P.p;
-                const int t = R.det_type[p];
-                if (!R.var_enabled[v * T + t]) continue;
-                int prev_end = -1;
-                if (spilled) {
-                    prev_end = (int)cur_s[p];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < LIVE; ++q)
-                        if (lp[q] == p) prev_end = le[q];
-                }
-                if (s < prev_end) continue;               // inside p's previous match (finditer)
-                const int e = P.e;
-                if (e < 0) continue;
-                if (spilled) {
-                    cur_s[p] = (uint32_t)e;
-                } else {
-                    int slot = -1;
-#pragma unroll
-                    for (int q = 0; q < LIVE; ++q)
-                        if (lp[q] == p) slot = q;
-                    if (slot < 0) {
-#pragma unroll
-                        for (int q = 0; q < LIVE; ++q)
-                            if (slot < 0 && le[q] <= s) slot = q;
-                    }
-                    if (slot >= 0) {
-#pragma unroll
-                        for (int q = 0; q < LIVE; ++q)
-                            if (q == slot) {
-                                lp[q] = p;
-                                le[q] = e;
-                            }
-                    } else {
-                        for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
-#pragma unroll
-                        for (int q = 0; q < LIVE; ++q)
-                            if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
-                        cur_s[p] = (uint32_t)e;
-                        spilled = true;
-                    }
-                }
-                const int xi = R.det_exidx[p];
-                const int lik = P.lik;
-                if (lik < minlik) {                        // invalid (-1) or below min_likelihood
-                    if (xi != 0xff) ex_valid &= ~(1u << xi);
-                    continue;
-                }
-                if (xi != 0xff) {
-#pragma unroll
-                    for (int x = 0; x < NE_MAX; ++x)
-                        if (x == xi) {
-                            ex_s[x] = s;
-                            ex_e[x] = e;
-                            ex_t[x] = t;
-                        }
-                    ex_valid |= 1u << xi;
-                }
-                const uint32_t x0 = R.excl_off[v * T + t], x1 = R.excl_off[v * T + t + 1];
-                bool excluded = false;
-                for (uint32_t q = x0; q < x1; ++q) {
-                    const int xt = R.excl_ids[q];
-#pragma unroll
-                    for (int x = 0; x < NE_MAX; ++x)
-                        if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
-                            excluded = true;
-                }
-                if (excluded) continue;
-                const bool better = best_e < 0 || e > best_e ||
-                                    (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
-                if (better) {
-                    best_e = e;
-                    best_t = t;
-                    best_lik = lik;
-                }
-            }
-            if (best_e >= 0 && s >= max_end) {
-                pii_span f;
-                f.utt = u;
-                f.start = (uint32_t)s;
-                f.end = (uint32_t)best_e;
-                f.info_type = (uint16_t)best_t;
-                f.likelihood = (uint8_t)best_lik;
-                f.flags = 0;
-                fdu[nf++] = f;
-                max_end = best_e;
-                out += (int64_t)(R.tok_off[best_t + 1] - R.tok_off[best_t]) - (best_e - s);
-            }
-        }
+        best_e = -1;
+    };
+    auto flush_utt = [&]() {
         if (nf) {
             n_find[u] = nf;
-            out_len[u] = (uint32_t)out;
+            out_len[u] = (uint32_t)(L + delta);
         }
+    };
+    for (uint32_t i0 = 0; i0 < np; i0 += 4) {
+        PairRes rr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (i0 + j < np) {
+                rr[j] = rl[i0 + j];
+            } else {
+                rr[j].p = 0;
+                rr[j].lik = -1;
+                rr[j].e = -1;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const PairRes P = rr[j];
+            if (P.e < 0) continue;
+            const PairLoc Lc = ll[i0 + j];
+            const int ps = (int)(Lc.s - Lc.ustart);
+            if (Lc.u != u) {
+                if (u != 0xffffffffu) {
+                    flush_start();
+                    flush_utt();
+                }
+                u = Lc.u;
+                v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
+                minlik = vmin[v];
+                L = (int)(Lc.uend - Lc.ustart);
+                fdu = fd + Lc.ustart / R.min_len;
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q) {
+                    lp[q] = -1;
+                    le[q] = -1;
+                }
+                spilled = false;
+                ex_valid = 0;
+                max_end = 0;
+                nf = 0;
+                delta = 0;
+                s = ps;
+            } else if (ps != s) {
+                flush_start();
+                s = ps;
+            }
+            const int p = P.p;
+            const int t = dtype[p];
+            if (!ven[v * T + t]) continue;
+            int prev_end = -1;
+            if (spilled) {
+                prev_end = (int)cur_s[p];
+            } else {
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q)
+                    if (lp[q] == p) prev_end = le[q];
+            }
+            if (s < prev_end) continue;               // inside p's previous match (finditer)
+            const int e = P.e;
+            if (spilled) {
+                cur_s[p] = (uint32_t)e;
+            } else {
+                int slot = -1;
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q)
+                    if (lp[q] == p) slot = q;
+                if (slot < 0) {
+#pragma unroll
+                    for (int q = 0; q < LIVE; ++q)
+                        if (slot < 0 && le[q] <= s) slot = q;
+                }
+                if (slot >= 0) {
+#pragma unroll
+                    for (int q = 0; q < LIVE; ++q)
+                        if (q == slot) {
+                            lp[q] = p;
+                            le[q] = e;
+                        }
+                } else {
+                    for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
+#pragma unroll
+                    for (int q = 0; q < LIVE; ++q)
+                        if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
+                    cur_s[p] = (uint32_t)e;
+                    spilled = true;
+                }
+            }
+            const int xi = dex[p];
+            const int lik = P.lik;
+            if (lik < minlik) {                        // invalid (-1) or below min_likelihood
+                if (xi != 0xff) ex_valid &= ~(1u << xi);
+                continue;
+            }
+            if (xi != 0xff) {
+#pragma unroll
+                for (int x = 0; x < NE_MAX; ++x)
+                    if (x == xi) {
+                        ex_s[x] = s;
+                        ex_e[x] = e;
+                        ex_t[x] = t;
+                    }
+                ex_valid |= 1u << xi;
+            }
+            const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
+            bool excluded = false;
+            for (uint32_t q = x0; q < x1; ++q) {
+                const int xt = xids[q];
+#pragma unroll
+                for (int x = 0; x < NE_MAX; ++x)
+                    if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
+                        excluded = true;
+            }
+            if (excluded) continue;
+            const bool better = best_e < 0 || e > best_e ||
+                                (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
+            if (better) {
+                best_e = e;
+                best_t = t;
+                best_lik = lik;
+            }
+        }
+    }
+    if (u != 0xffffffffu) {
+        flush_start();
+        flush_utt();
     }
 }
 
@@ -841,19 +973,21 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
 }
 
 // ---------------------------------------------------------------------------------- k_redact
-// Prefix-sum scatter.  A workgroup owns the utterances starting in REDACT_TILE_CHUNKS scan chunks:
-// one contiguous input range and one contiguous output range.  It stages the input bytes and the
-// "[INFO_TYPE]" token strings in LDS and builds a PIECE table (copy runs and tokens, sorted by output
-// offset; 1 + 2*findings pieces per utterance).  Every lane then assembles aligned 16-byte OUTPUT
-// blocks from LDS through the piece table -- one uniform code path -- and stores each with a single
-// dwordx4 store; only the two partial blocks at the range edges use byte stores.  Tiles that do not
-// fit fall back to a wavefront-per-utterance copy.
+// Prefix-sum scatter.  A workgroup owns REDACT_UTT consecutive utterances: one contiguous input range
+// and one contiguous output range.  It builds a PIECE table in LDS (copy runs and "[INFO_TYPE]"
+// tokens, sorted by output offset; 1 + 2*findings pieces per utterance) and copies the spans, then
+// a block -> piece table (each piece marks the first output block it can start, a prefix max fills
+// the rest).  Lane i assembles aligned 16-byte OUTPUT blocks i, i+256, ... so every load and store
+// instruction of a wavefront covers 1 KiB of consecutive bytes: a block inside one piece is two
+// aligned 16-byte source loads + a funnel shift (v_alignbyte), a block that straddles pieces ORs the
+// masked windows of each piece it touches.  Source bytes never pass through LDS.  Only the two
+// partial blocks at a tile's output edges use byte stores.  Tiles with more pieces than fit fall
+// back to a wavefront-per-utterance byte copy; tiles with more output blocks than the block table
+// holds look pieces up by binary search.
 constexpr int REDACT_BLOCK = 256;
-constexpr int REDACT_TILE_CHUNKS = 16;
-constexpr int STAGE_MAX = 16 * 1024;
-constexpr int TILE_UTT_MAX = 512;
-constexpr int PIECE_MAX = 1536;
-constexpr int TOK_MAX = 2048;
+constexpr int REDACT_UTT = 256;     // utterances per workgroup
+constexpr int PIECE_MAX = 1024;
+constexpr int BLK_MAX = 4096;       // output blocks (64 KiB) covered by the block -> piece table
 
 __device__ uint32_t redact_byte_slow(const RulesDev& R, const uint8_t* src, const pii_span* fdu, uint32_t nf,
                                      uint32_t rel) {
@@ -873,7 +1007,6 @@ __device__ uint32_t redact_byte_slow(const RulesDev& R, const uint8_t* src, cons
 
 __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ offs, uint32_t n_utt,
-                                                         const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
                                                          const pii_span* __restrict__ fd,
                                                          const uint32_t* __restrict__ n_find,
                                                          const uint64_t* __restrict__ out_offs,
@@ -881,42 +1014,32 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
                                                          const uint32_t* __restrict__ err, uint8_t* __restrict__ out,
                                                          pii_span* __restrict__ spans,
                                                          unsigned long long* __restrict__ hist) {
-    __shared__ __attribute__((aligned(16))) uint4 s_buf4[(STAGE_MAX + TOK_MAX) / 16 + 2];
     __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (tile relative)
-    __shared__ uint32_t s_psrc[PIECE_MAX + 1];     // piece source offset in s_buf
+    __shared__ uint64_t s_psrc[PIECE_MAX + 1];     // piece source: text position, or bit 63 | token offset
     __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
+    __shared__ uint16_t s_bp[BLK_MAX];             // output block -> piece holding its first byte
     __shared__ uint32_t sh_hist[256];
-    __shared__ int s_staged;
     if (*err != 0) return;
-    const uint32_t c0 = blockIdx.x * REDACT_TILE_CHUNKS;
-    const uint32_t c1 = min(c0 + REDACT_TILE_CHUNKS, n_chunks);
-    const uint32_t u0 = first_utt[c0], u1 = first_utt[c1];
-    if (u0 >= u1) return;
+    const uint32_t u0 = blockIdx.x * REDACT_UTT;
+    const uint32_t u1 = min(u0 + REDACT_UTT, n_utt);
     const uint32_t nu = u1 - u0;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int i = tid; i < 256; i += REDACT_BLOCK) sh_hist[i] = 0;
     const uint64_t base = offs[0];
-    const int64_t in_lo = (int64_t)offs[u0], in_hi = (int64_t)offs[u1];
     const int64_t out_lo = (int64_t)out_offs[u0], out_hi = (int64_t)out_offs[u1];
-    const int64_t mis = (int64_t)((uintptr_t)text & 15);
-    const int64_t a_lo = (in_lo + mis) >> 4;
-    const int64_t a_hi = in_hi > in_lo ? (in_hi - 1 + mis) >> 4 : a_lo;
-    const int64_t stage_pos = a_lo * 16 - mis;          // text position of s_buf[0]
-    const uint32_t tok_at = (uint32_t)((a_hi - a_lo + 1) * 16);
-    const uint32_t tok_len = R.tok_off[R.T];
-    bool staged = tok_at <= STAGE_MAX && tok_len <= TOK_MAX && nu <= TILE_UTT_MAX;
-    uint8_t* s_buf = reinterpret_cast<uint8_t*>(s_buf4);
-    // ---- piece counts + block scan ----
-    uint32_t cnt_i[2] = {0, 0};
-    if (staged) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const uint32_t i = tid * 2 + r;
-            cnt_i[r] = i < nu ? 1 + 2 * n_find[u0 + i] : 0;
-        }
+    // ---- per utterance: piece count, block scan ----
+    const bool mine = (uint32_t)tid < nu;
+    const uint32_t u = u0 + tid;
+    uint32_t nf = 0;
+    uint64_t s_abs = 0, o_abs = 0, sp_off = 0;
+    if (mine) {
+        nf = n_find[u];
+        s_abs = offs[u];
+        o_abs = out_offs[u];
+        sp_off = span_offs[u];
     }
-    uint32_t tsum = cnt_i[0] + cnt_i[1];
-    uint32_t incl = tsum;
+    const uint32_t cnt = mine ? 1 + 2 * nf : 0;
+    uint32_t incl = cnt;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t o = __shfl_up(incl, d);
         if (lane >= d) incl += o;
@@ -928,121 +1051,151 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
         if (w < wid) wpre += s_wsum[w];
         total_p += s_wsum[w];
     }
-    if (tid == 0) s_staged = staged && total_p <= PIECE_MAX;
-    __syncthreads();
-    staged = s_staged;
-    if (staged) {
-        const uint4* __restrict__ tp = reinterpret_cast<const uint4*>(text - mis);
-        for (int64_t a = a_lo + tid; a <= a_hi; a += REDACT_BLOCK) s_buf4[a - a_lo] = tp[a];
-        for (uint32_t i = tid; i < tok_len; i += REDACT_BLOCK) s_buf[tok_at + i] = R.tok_bytes[i];
-        uint32_t pb = wpre + incl - tsum;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const uint32_t i = tid * 2 + r;
-            if (i < nu) {
-                const uint32_t u = u0 + i;
-                const uint32_t nf = cnt_i[r] >> 1;
-                const uint32_t so = (uint32_t)((int64_t)offs[u] - stage_pos);
-                uint32_t po = (uint32_t)((int64_t)out_offs[u] - out_lo);
-                if (nf == 0) {
-                    s_pout[pb] = po;
-                    s_psrc[pb] = so;
-                    ++pb;
-                } else {
-                    const pii_span* fdu = fd + (offs[u] - base) / (uint64_t)R.min_len;
-                    uint32_t pin = 0;
-                    for (uint32_t f = 0; f < nf; ++f) {
-                        const pii_span F = fdu[f];
-                        s_pout[pb] = po;
-                        s_psrc[pb] = so + pin;
-                        po += F.start - pin;
-                        ++pb;
-                        const uint32_t t0 = R.tok_off[F.info_type];
-                        s_pout[pb] = po;
-                        s_psrc[pb] = tok_at + t0;
-                        po += R.tok_off[F.info_type + 1] - t0;
-                        ++pb;
-                        pin = F.end;
-                    }
+    const bool staged = total_p <= PIECE_MAX;
+    // ---- piece table + spans + histogram ----
+    if (mine) {
+        uint32_t pb = wpre + incl - cnt;
+        uint32_t po = (uint32_t)((int64_t)o_abs - out_lo);
+        const uint64_t so = s_abs;
+        if (nf == 0) {
+            if (staged) {
+                s_pout[pb] = po;
+                s_psrc[pb] = so;
+            }
+        } else {
+            const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
+            pii_span* sp = spans + sp_off;
+            uint32_t pin = 0;
+            for (uint32_t f = 0; f < nf; ++f) {
+                const pii_span F = fdu[f];
+                sp[f] = F;
+                if (F.info_type < 256) atomicAdd(&sh_hist[F.info_type], 1u);
+                const uint32_t t0 = R.tok_off[F.info_type];
+                if (staged) {
                     s_pout[pb] = po;
                     s_psrc[pb] = so + pin;
+                    po += F.start - pin;
+                    ++pb;
+                    s_pout[pb] = po;
+                    s_psrc[pb] = (1ull << 63) | t0;
+                    po += R.tok_off[F.info_type + 1] - t0;
                     ++pb;
                 }
+                pin = F.end;
+            }
+            if (staged) {
+                s_pout[pb] = po;
+                s_psrc[pb] = so + pin;
             }
         }
-        if (tid == 0) s_pout[total_p] = (uint32_t)(out_hi - out_lo);   // sentinel
     }
+    if (tid == 0 && staged) s_pout[total_p] = (uint32_t)(out_hi - out_lo);   // sentinel
     __syncthreads();
-    if (staged) {
-        const int64_t omis = (int64_t)((uintptr_t)out & 15);
+    const int64_t omis = (int64_t)((uintptr_t)out & 15);
+    const int64_t q_lo = (out_lo + omis) >> 4;
+    const int64_t q_hi = out_hi > out_lo ? (out_hi - 1 + omis) >> 4 : q_lo - 1;
+    const int64_t nblk = q_hi - q_lo + 1;
+    const bool table = staged && nblk > 0 && nblk <= BLK_MAX;
+    if (table) {
+        // block b's first valid byte is rf(b) = max(0, 16b - e0); piece(b) = max{p : pout[p] <= rf(b)}
+        const uint32_t e0 = (uint32_t)((out_lo + omis) - 16 * q_lo);
+        constexpr int PER = BLK_MAX / REDACT_BLOCK;
+        for (int i = tid; i < BLK_MAX; i += REDACT_BLOCK) s_bp[i] = 0;
+        __syncthreads();
+        for (uint32_t p = tid; p < total_p; p += REDACT_BLOCK) {
+            const uint32_t k = s_pout[p] == 0 ? 0u : (s_pout[p] + e0 + 15) >> 4;
+            const uint32_t kn = p + 1 == total_p ? 0xffffffffu : (s_pout[p + 1] == 0 ? 0u : (s_pout[p + 1] + e0 + 15) >> 4);
+            if (kn != k && k < (uint32_t)nblk) s_bp[k] = (uint16_t)p;      // last piece with this key
+        }
+        __syncthreads();
+        // prefix max over the block table: PER entries per lane, then across lanes
+        uint32_t m = 0;
+        for (int j = 0; j < PER; ++j) m = max(m, (uint32_t)s_bp[tid * PER + j]);
+        uint32_t incl_m = m;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl_m, d);
+            if (lane >= d) incl_m = max(incl_m, o);
+        }
+        if (lane == 63) s_wsum[wid] = incl_m;
+        __syncthreads();
+        uint32_t run = 0;
+        for (int w = 0; w < wid; ++w) run = max(run, s_wsum[w]);
+        const uint32_t excl_m = __shfl_up(incl_m, 1);
+        run = max(run, lane ? excl_m : 0u);
+        for (int j = 0; j < PER; ++j) {
+            run = max(run, (uint32_t)s_bp[tid * PER + j]);
+            s_bp[tid * PER + j] = (uint16_t)run;
+        }
+        __syncthreads();
+    }
+    if (staged && total_p > 0) {
         uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
-        const int64_t q_lo = (out_lo + omis) >> 4;
-        const int64_t q_hi = out_hi > out_lo ? (out_hi - 1 + omis) >> 4 : q_lo - 1;
         const int64_t span = out_hi - out_lo;
         for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
-            const int64_t r0 = q * 16 - omis - out_lo;
-            const uint32_t rs = (uint32_t)(r0 > 0 ? r0 : 0);
-            // last piece with s_pout <= rs
-            uint32_t lo_i = 0, hi_i = total_p - 1;
-            while (lo_i < hi_i) {
-                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                if (s_pout[mid] <= rs) lo_i = mid;
-                else hi_i = mid - 1;
-            }
-            uint32_t pi = lo_i;
-            uint32_t pstart = s_pout[pi], pend = s_pout[pi + 1], psrc = s_psrc[pi];
-            uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int64_t r = r0 + k;
-                uint32_t b = 0;
-                if (r >= 0 && r < span) {
-                    while ((uint32_t)r >= pend) {
-                        ++pi;
-                        pstart = pend;
-                        pend = s_pout[pi + 1];
-                        psrc = s_psrc[pi];
-                    }
-                    b = s_buf[psrc + ((uint32_t)r - pstart)];
+            const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
+            const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
+            const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
+            uint32_t pi;
+            if (table) {
+                pi = s_bp[q - q_lo];
+            } else {
+                const uint32_t rs = (uint32_t)(r0 + b_lo);
+                uint32_t lo_i = 0, hi_i = total_p - 1;       // last piece with s_pout <= rs
+                while (lo_i < hi_i) {
+                    const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                    if (s_pout[mid] <= rs) lo_i = mid;
+                    else hi_i = mid - 1;
                 }
-                w[k >> 2] |= b << (8 * (k & 3));
+                pi = lo_i;
             }
-            if (r0 >= 0 && r0 + 16 <= span) {
-                op[q] = make_uint4(w[0], w[1], w[2], w[3]);
+            uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
+            uint64_t qsrc = s_psrc[pi];
+            uint4 v = make_uint4(0, 0, 0, 0);
+            for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
+                const int lo = max(b_lo, (int)((int64_t)qs - r0));
+                const int hi = min(b_hi, (int)((int64_t)qe - r0));
+                if (hi > lo) {
+                    const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
+                    const uint8_t* src = (qsrc >> 63) ? R.tok_bytes + (uint32_t)qsrc + delta
+                                                      : text + (qsrc + delta);
+                    const uint4 w = load16(src, lo, hi);
+                    if (lo == 0 && hi == 16) {
+                        v = w;
+                    } else {
+                        v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
+                        v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
+                        v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
+                        v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
+                    }
+                }
+                if ((int64_t)qe >= r0 + b_hi) break;
+                ++pi;
+                qs = qe;
+                qe = s_pout[pi + 1];
+                qsrc = s_psrc[pi];
+            }
+            if (b_lo == 0 && b_hi == 16) {
+                op[q] = v;
             } else {
                 uint8_t* ob = out - omis + q * 16;
+                const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int64_t r = r0 + k;
-                    if (r >= 0 && r < span) ob[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-                }
+                for (int j = 0; j < 16; ++j)
+                    if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
             }
         }
-    } else {
-        // oversized tile: one wavefront per utterance, byte-granular
+    } else if (!staged) {
+        // too many pieces: one wavefront per utterance, byte-granular
         for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
-            const uint32_t u = u0 + i;
-            const uint64_t s_abs = offs[u];
-            const uint8_t* src = text + s_abs;
-            const uint32_t nf = n_find[u];
-            const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
-            uint8_t* dst = out + out_offs[u];
-            const uint32_t olen = (uint32_t)(out_offs[u + 1] - out_offs[u]);
+            const uint32_t uu = u0 + i;
+            const uint64_t sa = offs[uu];
+            const uint8_t* src = text + sa;
+            const uint32_t nfu = n_find[uu];
+            const pii_span* fdu = fd + (sa - base) / (uint64_t)R.min_len;
+            uint8_t* dst = out + out_offs[uu];
+            const uint32_t olen = (uint32_t)(out_offs[uu + 1] - out_offs[uu]);
             for (uint32_t rel = lane; rel < olen; rel += 64)
-                dst[rel] = (uint8_t)(nf ? redact_byte_slow(R, src, fdu, nf, rel) : src[rel]);
-        }
-    }
-    // spans + per-type histogram (findings are rare: one lane per utterance)
-    for (uint32_t i = tid; i < nu; i += REDACT_BLOCK) {
-        const uint32_t u = u0 + i;
-        const uint32_t nf = n_find[u];
-        if (nf == 0) continue;
-        const pii_span* fdu = fd + (offs[u] - base) / (uint64_t)R.min_len;
-        pii_span* sp = spans + span_offs[u];
-        for (uint32_t f = 0; f < nf; ++f) {
-            const pii_span F = fdu[f];
-            sp[f] = F;
-            if (F.info_type < 256) atomicAdd(&sh_hist[F.info_type], 1u);
+                dst[rel] = (uint8_t)(nfu ? redact_byte_slow(R, src, fdu, nfu, rel) : src[rel]);
         }
     }
     __syncthreads();
@@ -1051,6 +1204,31 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
 }
 
 __global__ void k_noop() {}
+
+// ------------------------------------------------------------------------------- LDS images
+// DFAs re-packed into a kernel's own pool (descriptor offsets rebased; each transition entry carries
+// the destination's flags in bits 14-15, see pii_device.h)
+struct DfaPool {
+    std::vector<uint16_t> trans;
+    std::vector<uint8_t> cmap;
+    std::vector<int32_t> desc;
+};
+bool add_dfa(DfaPool& dp, const int32_t* d, const uint16_t* trans, const uint8_t* flags, const uint8_t* cmap) {
+    const int32_t nc = d[3], ns = d[7];
+    if (ns > (int32_t)DFA_STATE_MASK + 1) return false;
+    int32_t nd[8];
+    std::memcpy(nd, d, sizeof(nd));
+    nd[0] = (int32_t)dp.trans.size();
+    nd[1] = 0;
+    nd[2] = (int32_t)dp.cmap.size();
+    for (size_t i = 0; i < (size_t)ns * nc; ++i) {
+        const uint16_t dst = trans[d[0] + i];
+        dp.trans.push_back((uint16_t)(dst | ((flags[d[1] + dst] & 3u) << 14)));
+    }
+    dp.cmap.insert(dp.cmap.end(), cmap + d[2], cmap + d[2] + 256);
+    dp.desc.insert(dp.desc.end(), nd, nd + 8);
+    return true;
+}
 
 // ------------------------------------------------------------------------------- blob parsing
 struct Section {
@@ -1089,6 +1267,29 @@ bool parse_blob(const uint8_t* p, size_t n, std::vector<Section>& out) {
 }  // namespace
 
 // ================================================================================ engine object
+struct DevImage {
+    LdsImage li{};
+    uint4* d = nullptr;
+};
+
+// packs `parts` (16-byte aligned sections) into one image and uploads it
+static bool make_image(const std::vector<std::pair<const void*, size_t>>& parts, DevImage& out) {
+    if (parts.size() > (size_t)IMG_MAX) return false;
+    size_t off = 0;
+    for (size_t i = 0; i < parts.size(); ++i) {
+        out.li.off[i] = (uint32_t)off;
+        off += (parts[i].second + 15) & ~(size_t)15;
+    }
+    if (off == 0) off = 16;
+    out.li.total = (uint32_t)off;
+    if (off > 160 * 1024) return false;
+    std::vector<uint8_t> img(off, 0);
+    for (size_t i = 0; i < parts.size(); ++i)
+        if (parts[i].second) std::memcpy(img.data() + out.li.off[i], parts[i].first, parts[i].second);
+    return hipMalloc(reinterpret_cast<void**>(&out.d), off) == hipSuccess &&
+           hipMemcpy(out.d, img.data(), off, hipMemcpyHostToDevice) == hipSuccess;
+}
+
 struct pii_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1101,8 +1302,7 @@ struct pii_engine {
     uint32_t n_slots = 0;
     int64_t ttl_us = 0;
     size_t scan_lds = 0;
-    void* d_rblob = nullptr;
-    RBOffs ro{};
+    DevImage img_first, img_eval, img_sel;     // per-kernel LDS images of the rule tables
     int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
@@ -1119,11 +1319,15 @@ struct pii_engine {
     uint32_t* first_utt = nullptr;
     uint32_t* lane_cnt = nullptr;
     uint64_t* bnd = nullptr;
-    Pair* pairs = nullptr;
+    PairLoc* ploc = nullptr;
+    PairRes* pres = nullptr;
     uint64_t pair_cap = 0;
     unsigned long long* pair_count = nullptr;
     uint64_t* lane_pair = nullptr;
     uint32_t* lane_np = nullptr;
+    uint32_t* matched = nullptr;
+    uint32_t* mcount = nullptr;   // matched pairs per k_pair_first segment
+    uint32_t n_seg = 0;
     struct Call {
         const uint8_t* text;
         const uint64_t* offs;
@@ -1182,6 +1386,16 @@ int grow(pii_engine* e, T*& p, size_t count) {
     return PII_OK;
 }
 
+int grow_pairs(pii_engine* e, uint64_t cap) {
+    if (cap >= (1ull << 32)) {
+        e->err = "pair queue beyond 2^32 entries; split the batch";
+        return PII_E_NOMEM;
+    }
+    int rc;
+    if ((rc = grow(e, e->ploc, cap)) || (rc = grow(e, e->pres, cap)) || (rc = grow(e, e->matched, cap))) return rc;
+    return PII_OK;
+}
+
 int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
     int rc = PII_OK;
     if (bytes > e->cap_bytes) {
@@ -1231,11 +1445,15 @@ int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out,
 int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
                  const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
                  uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info, hipStream_t st) {
+    if (total_bytes > PII_MAX_BATCH_BYTES) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
+        return PII_E_ARG;
+    }
     int rc = ensure_scratch(e, n_utt, total_bytes);
     if (rc) return rc;
     if (e->pair_cap < total_bytes / 16 + 4096) {
         const uint64_t cap = total_bytes / 16 + 4096;
-        if ((rc = grow(e, e->pairs, cap))) return rc;
+        if ((rc = grow_pairs(e, cap))) return rc;
         e->pair_cap = cap;
     }
     e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
@@ -1254,8 +1472,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_bounds<<<(n_utt + 255) / 256, 256, 0, st>>>(offs, n_utt, (int64_t)((uintptr_t)text & 63), e->bnd);
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
                 R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->ev, e->lane_cnt);
-            k_pairs<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, text, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt,
-                                                           role, e->kw, e->pairs, e->pair_cap, e->pair_count,
+            k_pairs<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt,
+                                                           role, e->kw, e->ploc, e->pres, e->pair_cap, e->pair_count,
                                                            e->lane_pair, e->lane_np, e->d_err);
         }
         HIPCHK(hipGetLastError());
@@ -1272,14 +1490,15 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
     if (n_utt > 0 && n_chunks > 0) {
-        const uint4* rb = static_cast<const uint4*>(e->d_rblob);
-        k_pair_first<<<e->n_cu * 2, 1024, e->ro.total, st>>>(rb, e->ro, text, offs, e->pair_count, e->pair_cap,
-                                                             e->pairs);
-        k_pair_eval<<<e->n_cu * 2, 1024, e->ro.total, st>>>(R, rb, e->ro, text, offs, role, ctx, e->pair_count,
-                                                            e->pair_cap, e->pairs);
-        k_select<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, offs, n_chunks, e->lane_pair, e->lane_np, e->pairs,
-                                                         e->pair_cap, role,
-                                                         ctx, e->fd, e->n_find, e->out_len);
+        k_pair_first<<<e->n_seg, PAIR_BLOCK, e->img_first.li.total, st>>>(
+            e->img_first.d, e->img_first.li, text, offs, e->pair_count, e->pair_cap, e->ploc, e->pres, e->matched,
+            e->mcount);
+        k_pair_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
+            e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, e->pair_count, e->pair_cap, e->matched,
+            e->mcount, e->n_seg, e->ploc, e->pres);
+        k_select<<<(n_chunks + 255) / 256, 256, e->img_sel.li.total, st>>>(
+            R, e->img_sel.d, e->img_sel.li, n_chunks, e->lane_pair, e->lane_np, e->ploc, e->pres, e->pair_cap, role,
+            ctx, e->fd, e->n_find, e->out_len);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[3], st));
@@ -1291,9 +1510,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
         if (n_chunks > 0)
-            k_redact<<<(n_chunks + REDACT_TILE_CHUNKS - 1) / REDACT_TILE_CHUNKS, REDACT_BLOCK, 0, st>>>(
-                R, text, offs, n_utt, e->first_utt, n_chunks, e->fd, e->n_find, out_offs, e->span_offs, e->d_err,
-                out, spans, e->hist);
+            k_redact<<<(n_utt + REDACT_UTT - 1) / REDACT_UTT, REDACT_BLOCK, 0, st>>>(
+                R, text, offs, n_utt, e->fd, e->n_find, out_offs, e->span_offs, e->d_err, out, spans, e->hist);
         k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
                                                           e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
@@ -1415,6 +1633,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         tok += "[" + e->names[t] + "]";
         tok_off[t + 1] = (uint32_t)tok.size();
     }
+    tok.append(32, '\0');     // k_redact reads aligned 16-byte windows past a token's end
     // one device buffer holding every table, 256-byte aligned sections
     struct Put {
         const void* src;
@@ -1435,8 +1654,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     size_t i_kacc = addsec("scan.k.accid"), i_kmin = add(k_acc_min.data(), k_acc_min.size() * 2);
     size_t i_dt = addsec("det.type"), i_dv = addsec("det.validator"), i_dl = addsec("det.lik"),
            i_dx = addsec("det.exidx"), i_fd = addsec("det.first_desc"), i_hr = addsec("hot.rule"),
-           i_hd = addsec("hot.dfa_desc"), i_pt = addsec("pool.trans"), i_pf = addsec("pool.flags"),
-           i_pc = addsec("pool.cmap"), i_ve = addsec("var.enabled"), i_vm = addsec("var.minlik"),
+           i_hd = addsec("hot.dfa_desc"), i_ve = addsec("var.enabled"), i_vm = addsec("var.minlik"),
            i_ro = addsec("var.rule_off"), i_ri = addsec("var.rule_ids"), i_eo = addsec("var.excl_off"),
            i_ei = addsec("var.excl_ids"), i_to = add(tok_off.data(), tok_off.size() * 4),
            i_tb = add(tok.data(), tok.size());
@@ -1462,9 +1680,6 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.first_desc = (const int32_t*)at(i_fd);
     R.hot_rule = (const int32_t*)at(i_hr);
     R.hot_desc = (const int32_t*)at(i_hd);
-    R.pool.trans = (const uint16_t*)at(i_pt);
-    R.pool.flags = (const uint8_t*)at(i_pf);
-    R.pool.cmap = (const uint8_t*)at(i_pc);
     R.var_enabled = (const uint8_t*)at(i_ve);
     R.var_minlik = (const uint8_t*)at(i_vm);
     R.rule_off = (const uint32_t*)at(i_ro);
@@ -1473,48 +1688,55 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.excl_ids = (const uint16_t*)at(i_ei);
     R.tok_off = (const uint32_t*)at(i_to);
     R.tok_bytes = (const uint8_t*)at(i_tb);
-    {   // LDS image for the pair kernels (RB_* order)
-        std::vector<std::pair<const void*, size_t>> parts(RB_N);
+    {   // per-kernel LDS images
         auto sec = [&](const char* nm) { return std::make_pair((const void*)find(nm)->data, (size_t)find(nm)->bytes); };
-        parts[RB_PTRANS] = sec("pool.trans");
-        parts[RB_PFLAGS] = sec("pool.flags");
-        parts[RB_PCMAP] = sec("pool.cmap");
-        parts[RB_FDESC] = sec("det.first_desc");
-        parts[RB_HDESC] = sec("hot.dfa_desc");
-        parts[RB_HRULE] = sec("hot.rule");
-        parts[RB_DTYPE] = sec("det.type");
-        parts[RB_DVAL] = sec("det.validator");
-        parts[RB_DLIK] = sec("det.lik");
-        parts[RB_DEX] = sec("det.exidx");
-        parts[RB_VEN] = sec("var.enabled");
-        parts[RB_VMIN] = sec("var.minlik");
-        parts[RB_ROFF] = sec("var.rule_off");
-        parts[RB_RIDS] = sec("var.rule_ids");
-        parts[RB_XOFF] = sec("var.excl_off");
-        parts[RB_XIDS] = sec("var.excl_ids");
-        parts[RB_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
-        parts[RB_AOFF] = sec("scan.d.acc_off");
-        parts[RB_AIDS] = sec("scan.d.acc_ids");
-        parts[RB_CMAP2] = sec("scan.cmap2");
-        size_t off = 0;
-        for (int i = 0; i < RB_N; ++i) {
-            e->ro.off[i] = (uint32_t)off;
-            off += (parts[i].second + 15) & ~(size_t)15;
-        }
-        e->ro.total = (uint32_t)off;
-        if (off > 160 * 1024) return fail("resolve tables do not fit in LDS");
-        std::vector<uint8_t> img(off, 0);
-        for (int i = 0; i < RB_N; ++i) std::memcpy(img.data() + e->ro.off[i], parts[i].first, parts[i].second);
-        if (hipMalloc(&e->d_rblob, off) != hipSuccess ||
-            hipMemcpy(e->d_rblob, img.data(), off, hipMemcpyHostToDevice) != hipSuccess)
-            return fail("resolve table upload failed");
-        if (off > 64 * 1024 &&
-            (hipFuncSetAttribute((const void*)k_pair_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)off) != hipSuccess ||
-             hipFuncSetAttribute((const void*)k_pair_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)off) != hipSuccess))
-            return fail("cannot raise LDS limit for the pair kernels");
+        const uint16_t* ptrans = (const uint16_t*)find("pool.trans")->data;
+        const uint8_t* pflags = (const uint8_t*)find("pool.flags")->data;
+        const uint8_t* pcmap = (const uint8_t*)find("pool.cmap")->data;
+        DfaPool fp, hp;
+        const int32_t* fdesc = (const int32_t*)find("det.first_desc")->data;
+        bool fits = true;
+        for (int p = 0; p < R.P; ++p) fits &= add_dfa(fp, fdesc + 8 * p, ptrans, pflags, pcmap);
+        const int32_t* hdesc = (const int32_t*)find("hot.dfa_desc")->data;
+        for (int h = 0; h < R.n_hot; ++h) fits &= add_dfa(hp, hdesc + 8 * h, ptrans, pflags, pcmap);
+        if (!fits) return fail("a FIRST/HOT automaton has more than 16384 states");
+        if (hp.desc.empty()) hp.desc.assign(8, 0);
+        auto vec = [](const auto& v) { return std::make_pair((const void*)v.data(), v.size() * sizeof(v[0])); };
+        std::vector<std::pair<const void*, size_t>> pf(FI_N), pe(EV_N), ps(SE_N);
+        pf[FI_TRANS] = vec(fp.trans);
+        pf[FI_CMAP] = vec(fp.cmap);
+        pf[FI_DESC] = vec(fp.desc);
+        pe[EV_TRANS] = vec(hp.trans);
+        pe[EV_CMAP] = vec(hp.cmap);
+        pe[EV_HDESC] = vec(hp.desc);
+        pe[EV_HRULE] = sec("hot.rule");
+        pe[EV_DTYPE] = sec("det.type");
+        pe[EV_DVAL] = sec("det.validator");
+        pe[EV_DLIK] = sec("det.lik");
+        pe[EV_ROFF] = sec("var.rule_off");
+        pe[EV_RIDS] = sec("var.rule_ids");
+        ps[SE_DTYPE] = sec("det.type");
+        ps[SE_VEN] = sec("var.enabled");
+        ps[SE_VMIN] = sec("var.minlik");
+        ps[SE_DEX] = sec("det.exidx");
+        ps[SE_XOFF] = sec("var.excl_off");
+        ps[SE_XIDS] = sec("var.excl_ids");
+        ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
+        if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
+            return fail("rule tables do not fit in LDS / upload failed");
+        const std::pair<const void*, const DevImage*> big[] = {
+            {(const void*)k_pair_first, &e->img_first}, {(const void*)k_pair_eval, &e->img_eval},
+            {(const void*)k_select, &e->img_sel}};
+        for (auto& kb : big)
+            if (kb.second->li.total > 64 * 1024 &&
+                hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
+                    hipSuccess)
+                return fail("cannot raise the LDS limit of a pair kernel");
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             e->n_cu = prop.multiProcessorCount;
+        e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
+        if (hipMalloc(&e->mcount, e->n_seg * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
     e->scan_lds = 512 + (size_t)((R.SD * R.CD + 1) / 2) * 4 + (size_t)((R.SK * R.CK + 1) / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
@@ -1546,8 +1768,9 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
 int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void* ptrs[] = {e->d_rules, e->d_rblob, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->pairs, e->pair_count, e->lane_pair, e->lane_np, e->kw, e->ctx, e->agg_v, e->commit,
+    void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->ploc, e->pres, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount,
+                    e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx};
     for (void* p : ptrs)
@@ -1613,7 +1836,7 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         // the (start, pattern) pair queue overflowed: grow it to the exact need and run the batch again
         // (the conversation context was not committed, so the re-run is idempotent)
         const uint64_t need = e->h_totals[3] + 4096;
-        int rc = grow(e, e->pairs, need);
+        int rc = grow_pairs(e, need);
         if (rc) return rc;
         e->pair_cap = need;
         const pii_engine::Call c = e->last;

@@ -36,6 +36,9 @@ extern "C" {
 /* return codes; the Python shim maps them onto the reference's error strings
  * ([DLP_PROCESSING_ERROR] {transcript} ..., main.py:752-773) */
 #define PII_OK 0
+/* largest batch (sum of row bytes) one call accepts: event/pair positions are 32-bit */
+#define PII_MAX_BATCH_BYTES 0xFFFF0000ull
+
 #define PII_E_ARG -1       /* bad argument / malformed offsets                              */
 #define PII_E_RULES -2     /* rules blob malformed or unsupported                           */
 #define PII_E_DEVICE -3    /* HIP runtime error                                             */
