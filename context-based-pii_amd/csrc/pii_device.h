@@ -37,9 +37,9 @@ __device__ __forceinline__ uint4 window16(const uint4& a, const uint4& b, uint32
 __device__ __forceinline__ uint4 load16(const uint8_t* src, int need_lo, int need_hi) {
     const uintptr_t a = (uintptr_t)src & ~(uintptr_t)15;
     const uint4* p = reinterpret_cast<const uint4*>(a);
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    const uint4 x = a + 16 > (uintptr_t)(src + need_lo) ? p[0] : z;
-    const uint4 y = a + 16 < (uintptr_t)(src + need_hi) ? p[1] : z;
+    uint4 x = make_uint4(0, 0, 0, 0), y = x;
+    if (a + 16 > (uintptr_t)(src + need_lo)) x = p[0];
+    if (a + 16 < (uintptr_t)(src + need_hi)) y = p[1];
     return window16(x, y, (uint32_t)((uintptr_t)src - a));
 }
 
@@ -229,30 +229,74 @@ struct Pool {
     const uint8_t* cmap;
 };
 
-// Anchored leftmost-first run of FIRST DFA `d` from byte s of text[0, L): returns the end `re`
-// would report for a match starting at s, or -1.  (compiler.build_first_dfa semantics.)
-__device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L) {
+// Anchored leftmost-first run of FIRST DFA `d` from byte s of text[0, L): the end `re` would report
+// for a match starting at s, or -1 (compiler.build_first_dfa semantics).  Split in two so a caller
+// can bound the lockstep cost: first_begin consumes at most one 16-byte window (the byte before s,
+// which picks the start state, then up to 15 bytes) and either finishes or leaves a resumable
+// {state, next position, last match end}; first_resume finishes it.
+struct FirstState {
+    uint32_t st;
+    int pos;    // next byte to consume
+    int last;   // end of the last match seen, -1 none
+};
+
+__device__ __forceinline__ int first_finish(const Pool& pool, const int32_t* d, const uint8_t* text, int L,
+                                            FirstState& r) {
     const uint16_t* tr = pool.trans + d[0];
     const uint8_t* cm = pool.cmap + d[2];
     const uint32_t nc = (uint32_t)d[3];
-    // the start state depends on the kind of text[s-1]: read it as the run's first window byte
-    constexpr uint32_t UNSET = 0xffffffffu;
-    uint32_t st = s == 0 ? (uint32_t)d[4] : UNSET;
-    const int lo = s == 0 ? 0 : s - 1;
-    int last = -1;
+    uint32_t st = r.st;
+    int last = r.last;
+    const int lo = r.pos;
     PII_FOR_BYTES(text, lo, L, {
-        if (st == UNSET) {
-            st = (uint32_t)(is_word(c) ? d[5] : d[6]);
-        } else {
-            const uint32_t e = tr[st * nc + cm[c]];
-            st = e & DFA_STATE_MASK;
-            if (e & 0x4000u) last = lo + i;
-            if (e & 0x8000u) return last;
-        }
+        const uint32_t e = tr[st * nc + cm[c]];
+        st = e & DFA_STATE_MASK;
+        if (e & 0x4000u) last = lo + i;
+        if (e & 0x8000u) return last;
     })
-    if (st == UNSET) st = (uint32_t)(is_word(text[lo]) ? d[5] : d[6]);     // s == L
     if (tr[st * nc + nc - 1] & 0x4000u) last = L;
     return last;
+}
+
+// returns the run's result (>= -1) when finished inside the first window, or -2 with `r` saved
+__device__ __forceinline__ int first_begin(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L,
+                                           FirstState& r) {
+    const uint16_t* tr = pool.trans + d[0];
+    const uint8_t* cm = pool.cmap + d[2];
+    const uint32_t nc = (uint32_t)d[3];
+    const int lo = s == 0 ? 0 : s - 1;
+    const int hi = L - lo < 16 ? L : lo + 16;
+    uint4 w = load16(text + lo, 0, hi - lo > 0 ? hi - lo : 1);
+    uint32_t st;
+    int j = s;
+    if (s == 0) {
+        st = (uint32_t)d[4];
+    } else {
+        st = (uint32_t)(is_word(w.x & 0xffu) ? d[5] : d[6]);
+        shr8(w);
+    }
+    int last = -1;
+    for (; j < hi; ++j) {
+        const uint32_t e = tr[st * nc + cm[w.x & 0xffu]];
+        st = e & DFA_STATE_MASK;
+        if (e & 0x4000u) last = j;
+        if (e & 0x8000u) return last;
+        shr8(w);
+    }
+    if (j >= L) {
+        if (tr[st * nc + nc - 1] & 0x4000u) last = L;
+        return last;
+    }
+    r.st = st;
+    r.pos = j;
+    r.last = last;
+    return -2;
+}
+
+__device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, const uint8_t* text, int s, int L) {
+    FirstState r;
+    const int e = first_begin(pool, d, text, s, L, r);
+    return e != -2 ? e : first_finish(pool, d, text, L, r);
 }
 
 // Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics)

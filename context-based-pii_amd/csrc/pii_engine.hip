@@ -41,7 +41,7 @@ constexpr int SCAN_BLOCK = 512;
 constexpr int CTX_BLOCK = 1024;
 constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
-constexpr uint32_t BYTES_PER_LANE = 512;
+constexpr uint32_t BYTES_PER_LANE = 1024;
 constexpr int KW_NONE = 0x7fff;
 
 enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8 };
@@ -55,8 +55,9 @@ struct Event {
 struct RulesDev {
     int P, G, T, V, SD, CD, d_start, SK, CK, k_start, n_hot, min_len;
     int kw_always_min, NE;
-    const uint16_t* cmap2;    // [256] classD | classK << 8
-    const uint16_t* td;       // [SD*CD] premultiplied next row | 0x8000 accept
+    uint32_t n_dacc, n_kacc;     // D / K accept sets
+    const uint32_t* cmap4;    // [256] 2*classD | 2*classK << 16 (byte offsets)
+    const uint16_t* td;       // [SD*CD] LDS byte address of the next row in k_scan | accept (bit 0)
     const uint16_t* tk;       // [SK*CK]
     const uint16_t* d_accid;  // [SD*CD]
     const uint32_t* d_acc_off;
@@ -106,13 +107,16 @@ __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* 
 
 // ------------------------------------------------------------------------------------- k_scan
 // Each lane owns the utterances whose START falls in its BYTES_PER_LANE slice of the batch, i.e. one
-// contiguous byte range, and walks it right to left in aligned 64-byte blocks (the next block is
-// prefetched while the current one is stepped).  Per 16 bytes the byte-class lookups are issued first
-// (independent of the automaton state), then the two automata take 16 dependent steps.  Utterance
-// boundaries are crossed in-stream: reaching an utterance's first byte applies the end-of-text pseudo
-// class (the "start of text" of the reverse automata) and resets the state.  A transition with bit 15
-// set appends {pos, previous D row, previous K row} to the lane's event region; nothing is written
-// per utterance (k_chunk_index wrote the defaults).
+// contiguous byte range [lo, hi], and walks it right to left in aligned 64-byte blocks (the next
+// block is prefetched while the current one is stepped).  Per 16 bytes the byte-class lookups are
+// issued first (independent of the automaton state), then the two automata take 16 dependent steps.
+// Utterance boundaries are crossed in-stream: reaching an utterance's first byte applies the
+// end-of-text pseudo class (the "start of text" of the reverse automata) and resets the state.
+// A step does no range test: the bytes of the edge blocks outside [lo, hi] are stepped too (the
+// boundary bit at hi + 1 -- a virtual one at the batch end -- resets the state before byte hi), and
+// only an event (rare) is range-checked.  A transition with bit 15 set appends {pos, D transition,
+// K transition} to the lane's event region; nothing is written per utterance (k_chunk_index wrote
+// the defaults).  Table entries are BYTE offsets (row * classes * 2) so one add forms an LDS address.
 template <int K>
 __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
     const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
@@ -121,8 +125,9 @@ __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
 
 // Utterance-start bitmap: bit k of word w <=> a non-empty utterance starts at text position
 // 64*w - mis + k - (word 0 offset), where mis = (text address) & 63, i.e. the bitmap words line up with
-// the scan's aligned 64-byte blocks.  The owner of a word (the first utterance starting in it) writes
-// it and zero-fills the words up to the next owner, so every word is written exactly once.
+// the scan's aligned 64-byte blocks; the batch end carries a bit too.  The owner of a word (the first
+// utterance starting in it) writes it and zero-fills the words up to the next owner, so every word is
+// written exactly once.
 __global__ void k_bounds(const uint64_t* __restrict__ offs, uint32_t n_utt, int64_t mis,
                          uint64_t* __restrict__ bnd) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -132,58 +137,76 @@ __global__ void k_bounds(const uint64_t* __restrict__ offs, uint32_t n_utt, int6
     if (u > 0 && (((int64_t)offs[u - 1] + mis) >> 6) == wu) return;      // not the owner
     uint64_t bits = 0;
     uint32_t v = u;
-    int64_t wn;
     for (;; ++v) {
         if (v == n_utt) {
-            wn = ((int64_t)offs[n_utt] - 1 + mis) >> 6;
-            wn = wn < wu ? wu + 1 : wn + 1;
-            break;
+            // batch end: its bit goes in its own word (this one or one past the zero-filled gap)
+            const int64_t se = (int64_t)offs[n_utt];
+            const int64_t we = (se + mis) >> 6;
+            if (we == wu) {
+                bits |= 1ull << ((se + mis) & 63);
+                bnd[wu - w0] = bits;
+            } else {
+                bnd[wu - w0] = bits;
+                for (int64_t w = wu + 1; w < we; ++w) bnd[w - w0] = 0;
+                bnd[we - w0] = 1ull << ((se + mis) & 63);
+            }
+            return;
         }
         const int64_t sv = (int64_t)offs[v];
         const int64_t wv = (sv + mis) >> 6;
         if (wv != wu) {
-            wn = wv;
-            break;
+            bnd[wu - w0] = bits;
+            for (int64_t w = wu + 1; w < wv; ++w) bnd[w - w0] = 0;
+            return;
         }
         if ((int64_t)offs[v + 1] > sv) bits |= 1ull << ((sv + mis) & 63);
     }
-    bnd[wu - w0] = bits;
-    for (int64_t w = wu + 1; w < wn; ++w) bnd[w - w0] = 0;
 }
 
-__device__ __forceinline__ void scan_bot(const RulesDev& R, const uint16_t* s_td, const uint16_t* s_tk,
-                                         uint32_t& sd, uint32_t& sk, uint32_t& cnt, Event* __restrict__ evl,
-                                         uint32_t pos) {
-    const uint32_t nd = s_td[sd + (uint32_t)(R.CD - 1)];
-    const uint32_t nk = s_tk[sk + (uint32_t)(R.CK - 1)];
-    if ((nd | nk) & 0x8000u) {
+// table entries are absolute LDS byte addresses of the next row, bit 0 = accept (scan_tables); k_scan
+// has no static LDS, so its dynamic region starts at LDS address 0 and an entry IS the address
+constexpr uint32_t SCAN_TD_BASE = 1024;     // after the 256-entry class map
+typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
+__device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
+    return *reinterpret_cast<lds_u16_t*>((size_t)addr);
+}
+
+__device__ __forceinline__ void scan_emit(Event* __restrict__ evl, uint32_t& cnt, int64_t pos, int64_t lo_r,
+                                          int64_t hi_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
+    if (pos >= lo_r && pos <= hi_r) {
         Event e;
-        e.pos = pos;
-        e.sd = (uint16_t)(sd + (uint32_t)(R.CD - 1));
-        e.sk = (uint16_t)(sk + (uint32_t)(R.CK - 1));
+        e.pos = (uint32_t)pos;
+        e.sd = (uint16_t)((ad - SCAN_TD_BASE) >> 1);     // transition index (row * CD + class)
+        e.sk = (uint16_t)((ak - tk_base) >> 1);
         evl[cnt++] = e;
     }
-    sd = (uint32_t)R.d_start;
-    sk = (uint32_t)R.k_start;
+}
+
+// utterance start at pos: the end-of-text pseudo step, then reset
+__device__ __forceinline__ void scan_bot(const uint8_t* lds, uint32_t eot_d, uint32_t eot_k, uint32_t d_start,
+                                         uint32_t k_start, uint32_t tk_base, uint32_t& sd, uint32_t& sk,
+                                         uint32_t& cnt, Event* __restrict__ evl, int64_t pos, int64_t lo_r,
+                                         int64_t hi_r) {
+    (void)lds;
+    const uint32_t nd = lds_u16(sd + eot_d);
+    const uint32_t nk = lds_u16(sk + eot_k);
+    if ((nd | nk) & 1u) scan_emit(evl, cnt, pos, lo_r, hi_r, sd + eot_d, sk + eot_k, tk_base);
+    sd = d_start;
+    sk = k_start;
 }
 
 #define SCAN_STEP(K, OFF)                                                                         \
     {                                                                                             \
-        const int64_t jj = jc + (K);                                                             \
-        const uint32_t nd = s_td[sd + (cc[K] & 0xffu)];                                         \
-        const uint32_t nk = s_tk[sk + (cc[K] >> 8)];                                            \
-        if (jj >= lo && jj <= hi) {                                                               \
-            if (__builtin_expect(((nd | nk) & 0x8000u) != 0, 0)) {                                \
-                Event e;                                                                          \
-                e.pos = (uint32_t)(jj + 1 - base);                                                \
-                e.sd = (uint16_t)(sd + (cc[K] & 0xffu));                                          \
-                e.sk = (uint16_t)(sk + (cc[K] >> 8));                                             \
-                evl[cnt++] = e;                                                                   \
-            }                                                                                     \
-            sd = nd & 0x7fffu;                                                                    \
-            sk = nk & 0x7fffu;                                                                    \
-            if (__builtin_expect((bits >> ((OFF) + (K))) & 1, 0))                                 \
-                scan_bot(R, s_td, s_tk, sd, sk, cnt, evl, (uint32_t)(jj - base));                 \
+        const uint32_t ad = sd + (cc[K] & 0xffffu);                                               \
+        const uint32_t ak = sk + (cc[K] >> 16);                                                   \
+        const uint32_t nd = lds_u16(ad);                                                          \
+        const uint32_t nk = lds_u16(ak);                                                          \
+        sd = nd & 0xfffeu;                                                                        \
+        sk = nk & 0xfffeu;                                                                        \
+        if (__builtin_expect((((nd | nk) & 1u) | (b16 & (1u << (K)))) != 0, 0)) {                 \
+            if ((nd | nk) & 1u) scan_emit(evl, cnt, bpos + (OFF) + (K) + 1, lo_r, hi_r, ad, ak, tk_base); \
+            if (b16 & (1u << (K)))                                                                \
+                scan_bot(lds, eot_d, eot_k, d_start, k_start, tk_base, sd, sk, cnt, evl, bpos + (OFF) + (K), lo_r, hi_r); \
         }                                                                                         \
     }
 
@@ -209,7 +232,7 @@ __device__ __forceinline__ void scan_bot(const RulesDev& R, const uint16_t* s_td
     {                                                                                             \
         uint32_t cc[16];                                                                          \
         SCAN_CLASSES(W)                                                                           \
-        const int64_t jc = blk * 64 - mis + (OFF);                                                \
+        const uint32_t b16 = (uint32_t)(bits >> (OFF)) & 0xffffu;                                 \
         SCAN_STEP(15, OFF) SCAN_STEP(14, OFF) SCAN_STEP(13, OFF) SCAN_STEP(12, OFF)               \
         SCAN_STEP(11, OFF) SCAN_STEP(10, OFF) SCAN_STEP(9, OFF) SCAN_STEP(8, OFF)                 \
         SCAN_STEP(7, OFF) SCAN_STEP(6, OFF) SCAN_STEP(5, OFF) SCAN_STEP(4, OFF)                   \
@@ -222,18 +245,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
                                                      const uint64_t* __restrict__ bnd, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
-    uint16_t* s_cmap = reinterpret_cast<uint16_t*>(smem32);
+    uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
     const int nd_words = (R.SD * R.CD + 1) / 2;
     const int nk_words = (R.SK * R.CK + 1) / 2;
-    uint16_t* s_td = s_cmap + 256;
-    uint16_t* s_tk = s_td + nd_words * 2;
+    const uint8_t* lds = reinterpret_cast<const uint8_t*>(smem32);
+    const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)nd_words * 4;
     {
-        const uint32_t* g_cmap = reinterpret_cast<const uint32_t*>(R.cmap2);
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
         const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
-        uint32_t* d_td = smem32 + 128;
+        uint32_t* d_td = smem32 + 256;
         uint32_t* d_tk = d_td + nd_words;
-        for (int i = threadIdx.x; i < 128; i += blockDim.x) smem32[i] = g_cmap[i];
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
         for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
         for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
     }
@@ -244,17 +266,27 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
     const int64_t base = (int64_t)offs[0];
     const int64_t lo = (int64_t)offs[u0];   // lane range [lo, hi]
     const int64_t hi = (int64_t)offs[u1] - 1;
+    const int64_t end = (int64_t)offs[n_utt];
     uint32_t cnt = 0;
     if (hi >= lo) {
         Event* __restrict__ evl = ev + (lo - base);
-        uint32_t sd = (uint32_t)R.d_start, sk = (uint32_t)R.k_start;
+        const int64_t lo_r = lo - base, hi_r = hi - base;
+        const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
+        const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
+        uint32_t sd = d_start, sk = k_start;
         // aligned 64-byte blocks in ADDRESS space: block b covers positions [64b - mis, 64b - mis + 64)
         const int64_t mis = (int64_t)((uintptr_t)text & 63);
         const uint4* __restrict__ tp = reinterpret_cast<const uint4*>(text - mis);
         const int64_t b0 = (base + mis) >> 6;
         const int64_t b_hi = (hi + mis) >> 6;
         const int64_t b_lo = (lo + mis) >> 6;
-        uint4 n0 = tp[4 * b_hi], n1 = tp[4 * b_hi + 1], n2 = tp[4 * b_hi + 2], n3 = tp[4 * b_hi + 3];
+        // the top block: only chunks holding a batch byte are read (the rest step as zero bytes
+        // before the end-of-batch / next-utterance reset)
+        const int64_t q_end = (end - 1 + mis) >> 4;               // last chunk with a batch byte
+        uint4 n0 = tp[4 * b_hi], n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
+        if (4 * b_hi + 1 <= q_end) n1 = tp[4 * b_hi + 1];
+        if (4 * b_hi + 2 <= q_end) n2 = tp[4 * b_hi + 2];
+        if (4 * b_hi + 3 <= q_end) n3 = tp[4 * b_hi + 3];
         uint64_t nb = bnd[b_hi - b0];
         for (int64_t blk = b_hi; blk >= b_lo; --blk) {
             const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
@@ -267,6 +299,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
                 n3 = tp[q + 3];
                 nb = bnd[blk - 1 - b0];
             }
+            const int64_t bpos = blk * 64 - mis - base;        // position of the block's byte 0
             SCAN_SUB(w3, 48)
             SCAN_SUB(w2, 32)
             SCAN_SUB(w1, 16)
@@ -411,16 +444,21 @@ __global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int16_t* _
 //   k_pair_first per pair: anchored leftmost-first run -> end (or -1)      [lockstep DFA runs]
 //   k_pair_eval  per matched pair: validator + hotword windows of the row's context variant -> likelihood
 //   k_select     per scan lane: finditer skipping, exclusion, overlap resolution -> kept findings
-struct PairLoc {       // where a candidate is (16 B: one dwordx4)
+struct EvLoc {         // where an event's candidates start (16 B: one dwordx4), one per event
     uint32_t u;        // utterance
     uint32_t s;        // candidate start, relative to the batch base
     uint32_t ustart;   // utterance start, relative to the batch base
     uint32_t uend;     // utterance end, relative to the batch base
 };
-struct PairRes {       // what it turned into (8 B)
+struct EvPairs {       // an event's block of the pair queue (8 B), expanded by k_expand
+    uint32_t first;    // first pair index
+    uint16_t acc;      // D accept set
+    uint16_t n;        // pairs (patterns in the accept set)
+};
+struct PairRes {       // one (start, pattern) candidate (8 B); its FIRST end lives in pend[] (4 B)
+    uint32_t ev;       // dense event index -> EvLoc
     uint16_t p;        // detector pattern
     int16_t lik;       // likelihood after validation + hotwords; -1 = invalid
-    int32_t e;         // leftmost-first match end, relative to the utterance start; -1 = no match
 };
 
 // LDS images of rule tables, one per kernel (only what that kernel reads, so the pair kernels keep
@@ -436,38 +474,87 @@ enum { SE_DTYPE, SE_VEN, SE_VMIN, SE_DEX, SE_XOFF, SE_XIDS, SE_TOKOFF, SE_N };
 
 constexpr int PAIR_BLOCK = 1024;
 
-// pair-queue segment of workgroup g in k_pair_first / k_pair_eval: [g*seg, (g+1)*seg)
-__device__ __forceinline__ uint64_t pair_segment(uint64_t n, uint32_t nseg) {
-    const uint64_t per = (n + nseg - 1) / nseg;
-    return (per + PAIR_BLOCK - 1) / PAIR_BLOCK * PAIR_BLOCK;
+constexpr int PAIR_WAVES = PAIR_BLOCK / 64;
+
+// pair-queue segment of wavefront w of k_pair_first (and of its matched / continuation lists):
+// [w*seg, (w+1)*seg), seg a multiple of 64
+__device__ __forceinline__ uint64_t pair_segment(uint64_t n, uint32_t nwaves) {
+    const uint64_t per = (n + nwaves - 1) / nwaves;
+    return (per + 63) / 64 * 64;
 }
 
-__global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint64_t* __restrict__ offs,
+struct FirstCont {     // a FIRST run still alive after its first window
+    uint32_t i;        // pair
+    uint32_t st;
+    int32_t pos;       // next byte, relative to the utterance start
+    int32_t last;
+};
+
+// Each wavefront first stages the offsets (u32, batch relative) and roles of the utterances its 64
+// lanes cover into LDS with coalesced loads, so the per-lane walks (event -> utterance) read LDS
+// instead of issuing dependent, uncoalesced global loads.  A wavefront whose lanes cover more than
+// PAIRS_UCAP utterances (very short rows) walks global memory instead.
+constexpr int PAIRS_BLOCK = 256;
+constexpr int PAIRS_UCAP = 1024;
+
+// Two launches: WRITE = false counts each lane's pairs (and records the AGENT rows' keyword groups),
+// an exclusive scan of the counts gives every lane its block of the queue (lane order, no atomics),
+// WRITE = true fills the blocks.
+template <bool WRITE>
+__global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const uint64_t* __restrict__ offs,
                                                const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
                                                const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
                                                const uint8_t* __restrict__ role, int16_t* __restrict__ kw,
-                                               PairLoc* __restrict__ ploc, PairRes* __restrict__ pres,
-                                               uint64_t pair_cap, unsigned long long* __restrict__ pair_count,
-                                               uint64_t* __restrict__ lane_pair, uint32_t* __restrict__ lane_np,
-                                               uint32_t* __restrict__ err) {
+                                               EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
+                                               uint64_t pair_cap, uint64_t ev_cap,
+                                               const uint64_t* __restrict__ lane_pair,
+                                               const uint64_t* __restrict__ lane_ev,
+                                               uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
+    __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
+    __shared__ uint32_t s_acc_off[256];
+    __shared__ uint16_t s_kmin[256];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const bool valid = c < n_chunks;
-    const uint32_t cnt = valid ? lane_cnt[c] : 0u;
     const int64_t base = (int64_t)offs[0];
+    // small accept-set tables (<= 256 sets; larger rule sets read them from global memory)
+    const uint32_t n_dacc = R.n_dacc, n_kacc = R.n_kacc;
+    for (uint32_t i = threadIdx.x; i <= n_dacc && i < 256; i += PAIRS_BLOCK) s_acc_off[i] = R.d_acc_off[i];
+    for (uint32_t i = threadIdx.x; i < n_kacc && i < 256; i += PAIRS_BLOCK) s_kmin[i] = R.k_acc_min[i];
+    // the wavefront's utterances [U0, U1]
+    const uint32_t cw0 = c - lane;
+    const uint32_t cw1 = min(cw0 + 64, n_chunks);
+    const uint32_t U0 = cw0 < n_chunks ? first_utt[cw0] : 0u;
+    const uint32_t U1 = cw0 < n_chunks ? first_utt[cw1] : 0u;
+    const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
+    uint32_t* so = s_off[wv];
+    uint8_t* sr = s_role[wv];
+    if (staged && cw0 < n_chunks) {
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)((int64_t)offs[U0 + k] - base);
+        for (uint32_t k = lane; k < U1 - U0; k += 64) sr[k] = role[U0 + k];
+    }
+    __syncthreads();
+    const bool small_acc = n_dacc < 256 && n_kacc <= 256;
+    auto acc_off = [&](uint32_t a) { return small_acc ? s_acc_off[a] : R.d_acc_off[a]; };
+    auto kmin = [&](uint32_t a) { return small_acc ? (uint32_t)s_kmin[a] : (uint32_t)R.k_acc_min[a]; };
+    auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : (int64_t)offs[u] - base; };
+    auto uagent = [&](int64_t u) { return (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT; };
+
+    const uint32_t cnt = valid ? lane_cnt[c] : 0u;
     const Event* evl = nullptr;
     int64_t u_top = 0;
     if (cnt) {
         const uint32_t u0 = first_utt[c];
-        evl = ev + ((int64_t)offs[u0] - base);
+        evl = ev + uoff(u0);
         u_top = (int64_t)first_utt[c + 1] - 1;
     }
-    // pass 1: count pairs, keyword groups of AGENT rows
-    uint32_t np = 0;
-    {
+    if (!WRITE) {
+        // count pairs, keyword groups of AGENT rows
+        uint32_t np = 0;
         int64_t u = u_top;
-        int64_t s_u = cnt ? (int64_t)offs[u] - base : 0;
-        bool agent = cnt ? role[u] == PII_ROLE_AGENT : false;
+        int64_t s_u = cnt ? uoff(u) : 0;
+        bool agent = cnt ? uagent(u) : false;
         int g = KW_NONE;
         for (uint32_t k = 0; k < cnt; ++k) {
             const Event E = evl[k];
@@ -476,65 +563,85 @@ __global__ __launch_bounds__(256) void k_pairs(const RulesDev R, const uint64_t*
                 if (g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
                 g = KW_NONE;
                 --u;
-                s_u = (int64_t)offs[u] - base;
-                agent = role[u] == PII_ROLE_AGENT;
+                s_u = uoff(u);
+                agent = uagent(u);
             }
             const uint32_t acc = R.d_accid[E.sd];
-            np += R.d_acc_off[acc + 1] - R.d_acc_off[acc];
+            np += acc_off(acc + 1) - acc_off(acc);
             if (agent) {
                 const uint32_t a = R.k_accid[E.sk];
-                if (a) g = min(g, (int)R.k_acc_min[a]);
+                if (a) g = min(g, (int)kmin(a));
             }
         }
         if (cnt && g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
+        if (valid) lane_np[c] = np;
+        return;
     }
-    // wave-aggregated allocation
-    uint32_t incl = np;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d);
-        if (lane >= d) incl += o;
-    }
-    unsigned long long wbase = 0;
-    if (lane == 63 && incl) wbase = atomicAdd(pair_count, (unsigned long long)incl);
-    wbase = __shfl(wbase, 63);
-    const uint64_t my = wbase + (incl - np);
-    if (valid) {
-        lane_pair[c] = my;
-        lane_np[c] = np;
-    }
-    if (np == 0) return;
-    if (my + np > pair_cap) {
+    if (!valid) return;
+    const uint32_t np = lane_np[c];
+    const uint64_t my = lane_pair[c];
+    const uint64_t evb = lane_ev[c];
+    if (cnt == 0) return;                 // (every event gets its EvPairs record, even with no pairs)
+    if (my + np > pair_cap || evb + cnt > ev_cap) {
         atomicOr(err, (uint32_t)ERR_QUEUE);
         return;
     }
     // pass 2: write back to front -> ascending by start
     uint64_t w = my + np;
     int64_t u = u_top;
-    int64_t s_u = (int64_t)offs[u] - base;
-    int64_t e_u = (int64_t)offs[u + 1] - base;
+    int64_t s_u = uoff(u);
+    int64_t e_u = uoff(u + 1);
     for (uint32_t k = 0; k < cnt; ++k) {
         const Event E = evl[k];
         const int64_t pos = E.pos;
         while (pos < s_u) {
             --u;
             e_u = s_u;
-            s_u = (int64_t)offs[u] - base;
+            s_u = uoff(u);
         }
         const uint32_t acc = R.d_accid[E.sd];
-        const uint32_t a0 = R.d_acc_off[acc], a1 = R.d_acc_off[acc + 1];
+        const uint32_t a0 = acc_off(acc), a1 = acc_off(acc + 1);
         w -= a1 - a0;
-        PairLoc Lc;
+        EvPairs ep;
+        ep.first = (uint32_t)w;
+        ep.acc = (uint16_t)acc;
+        ep.n = (uint16_t)(a1 - a0);
+        evpairs[evb + k] = ep;
+        if (a1 == a0) continue;
+        EvLoc Lc;
         Lc.u = (uint32_t)u;
         Lc.s = (uint32_t)pos;
         Lc.ustart = (uint32_t)s_u;
         Lc.uend = (uint32_t)e_u;
-        for (uint32_t i = a0; i < a1; ++i) {
+        evloc[evb + k] = Lc;
+    }
+}
+
+// one thread per event: its (start, pattern) pairs, accept-set order (excluders first)
+__global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs* __restrict__ evpairs,
+                                                const uint64_t* __restrict__ ev_count, const uint32_t* __restrict__ err,
+                                                PairRes* __restrict__ pres) {
+    __shared__ uint32_t s_off[257];
+    if (*err & ERR_QUEUE) return;           // a queue overflowed: records are incomplete, the batch re-runs
+    __shared__ uint16_t s_ids[2048];
+    const uint32_t n_dacc = R.n_dacc;
+    const bool small = n_dacc < 256 && R.d_acc_off[n_dacc] <= 2048;
+    if (small) {
+        for (uint32_t i = threadIdx.x; i <= n_dacc; i += blockDim.x) s_off[i] = R.d_acc_off[i];
+        for (uint32_t i = threadIdx.x; i < R.d_acc_off[n_dacc]; i += blockDim.x) s_ids[i] = R.d_acc_ids[i];
+    }
+    __syncthreads();
+    const uint64_t n = *ev_count;
+    for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+        const EvPairs ep = evpairs[k];
+        if (ep.n == 0) continue;
+        const uint32_t a0 = small ? s_off[ep.acc] : R.d_acc_off[ep.acc];
+        for (uint32_t i = 0; i < ep.n; ++i) {
             PairRes P;
-            P.p = R.d_acc_ids[i];
+            P.ev = (uint32_t)k;
+            P.p = small ? s_ids[a0 + i] : R.d_acc_ids[a0 + i];
             P.lik = -1;
-            P.e = -1;
-            ploc[w + (i - a0)] = Lc;
-            pres[w + (i - a0)] = P;
+            pres[ep.first + i] = P;
         }
     }
 }
@@ -545,76 +652,94 @@ __device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ i
     return reinterpret_cast<const uint8_t*>(lds4);
 }
 
-// per pair: anchored leftmost-first run.  Workgroup g owns one contiguous segment of the queue and
-// compacts its matched pairs, in queue order, into the same segment of `matched` (no global atomics).
+// per pair: anchored leftmost-first run.  Each wavefront owns one contiguous segment of the queue
+// (no workgroup barriers while it runs) and compacts, by ballot, its matched pairs into the same
+// segment of `matched` and the runs still alive after one 16-byte window into the same segment of
+// `cont`.  The workgroup then finishes all its continuations densely, so one long run no longer holds
+// 63 idle lanes; their matches are appended through LDS counters.
 __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
                                                            const uint8_t* __restrict__ text0,
                                                            const uint64_t* __restrict__ offs,
                                                            const unsigned long long* __restrict__ pair_count,
-                                                           uint64_t pair_cap, const PairLoc* __restrict__ ploc,
-                                                           PairRes* __restrict__ pres, uint32_t* __restrict__ matched,
-                                                           uint32_t* __restrict__ mcount) {
+                                                           uint64_t pair_cap, const EvLoc* __restrict__ evloc,
+                                                           const PairRes* __restrict__ pres,
+                                                           int32_t* __restrict__ pend, uint32_t* __restrict__ matched,
+                                                           FirstCont* __restrict__ cont,
+                                                           uint32_t* __restrict__ mcount,
+                                                           const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    __shared__ uint32_t s_wcnt[PAIR_BLOCK / 64];
-    __shared__ uint32_t s_bucket[P_MAX], s_bstart[P_MAX];
-    __shared__ uint16_t s_perm[PAIR_BLOCK];
+    __shared__ uint32_t s_mc[PAIR_WAVES], s_cc[PAIR_WAVES + 1];
+    if (*err & ERR_QUEUE) {
+        if (threadIdx.x < PAIR_WAVES) mcount[blockIdx.x * PAIR_WAVES + threadIdx.x] = 0;
+        return;
+    }
     const uint8_t* lb = load_image(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[FI_TRANS]), lb + li.off[FI_CMAP]};
     const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + li.off[FI_DESC]);
     const uint64_t n = min((uint64_t)*pair_count, pair_cap);
     const uint8_t* text = text0 + offs[0];     // pair positions are relative to the batch base
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t seg = pair_segment(n, gridDim.x);
-    const uint64_t lo = blockIdx.x * seg, hi = min(n, lo + seg);
-    uint32_t cnt = 0;
-    for (uint64_t b = lo; b < hi; b += PAIR_BLOCK) {       // uniform trip count in the workgroup
-        // counting sort of the batch by pattern, so a wavefront runs one automaton on runs of
-        // similar length (its step count is the longest run among its lanes)
-        if (threadIdx.x < P_MAX) s_bucket[threadIdx.x] = 0;
-        __syncthreads();
-        const uint64_t i0 = b + threadIdx.x;
-        uint32_t p0 = 0, rank = 0;
-        if (i0 < hi) {
-            p0 = pres[i0].p;
-            rank = atomicAdd(&s_bucket[p0], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {                               // exclusive scan of the P_MAX buckets
-            const uint32_t v = s_bucket[threadIdx.x];
-            uint32_t inc = v;
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = __shfl_up(inc, d);
-                if (lane >= d) inc += o;
-            }
-            s_bstart[threadIdx.x] = inc - v;
-        }
-        __syncthreads();
-        if (i0 < hi) s_perm[s_bstart[p0] + rank] = (uint16_t)threadIdx.x;
-        __syncthreads();
-        const uint32_t nb = (uint32_t)min((uint64_t)PAIR_BLOCK, hi - b);
-        const uint64_t i = b + ((uint32_t)threadIdx.x < nb ? s_perm[threadIdx.x] : 0u);
+    const uint32_t gw = blockIdx.x * PAIR_WAVES + wave;
+    const uint64_t seg = pair_segment(n, gridDim.x * PAIR_WAVES);
+    const uint64_t lo = gw * seg, hi = min(n, lo + seg);
+    const uint64_t lanemask = (1ull << lane) - 1;
+    uint32_t mc = 0, cc = 0;
+    for (uint64_t b = lo; b < hi; b += 64) {
+        const uint64_t i = b + lane;
         int e = -1;
-        if ((uint32_t)threadIdx.x < nb) {
-            const PairLoc L = ploc[i];
-            const int p = pres[i].p;
-            const uint8_t* t0 = text + L.ustart;
-            e = first_run(pool, fdesc + 8 * p, t0, (int)(L.s - L.ustart), (int)(L.uend - L.ustart));
-            if (e >= 0) pres[i].e = e;
+        FirstState r;
+        if (i < hi) {
+            const PairRes P = pres[i];
+            const EvLoc L = evloc[P.ev];
+            e = first_begin(pool, fdesc + 8 * P.p, text + L.ustart, (int)(L.s - L.ustart), (int)(L.uend - L.ustart), r);
+            pend[i] = e < 0 ? -1 : e;                 // still-running runs (-2) are completed below
         }
-        const uint64_t m = __ballot(e >= 0);
-        if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < PAIR_BLOCK / 64; ++w) {
-            const uint32_t c = s_wcnt[w];
-            before += w < wave ? c : 0u;
-            total += c;
+        const uint64_t mm = __ballot(e >= 0), mcn = __ballot(e == -2);
+        if (e >= 0) matched[lo + mc + __popcll(mm & lanemask)] = (uint32_t)i;
+        if (e == -2) {
+            FirstCont C;
+            C.i = (uint32_t)i;
+            C.st = r.st;
+            C.pos = r.pos;
+            C.last = r.last;
+            cont[lo + cc + __popcll(mcn & lanemask)] = C;
         }
-        if (e >= 0) matched[lo + cnt + before + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)i;
-        cnt += total;
+        mc += __popcll(mm);
+        cc += __popcll(mcn);
     }
-    if (threadIdx.x == 0) mcount[blockIdx.x] = cnt;
+    if (lane == 0) {
+        s_mc[wave] = mc;
+        s_cc[wave] = cc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < PAIR_WAVES; ++w) {
+            const uint32_t c = s_cc[w];
+            s_cc[w] = run;
+            run += c;
+        }
+        s_cc[PAIR_WAVES] = run;
+    }
+    __syncthreads();
+    // continuations of the whole workgroup, densely
+    const uint32_t total = s_cc[PAIR_WAVES];
+    for (uint32_t k = threadIdx.x; k < total; k += PAIR_BLOCK) {
+        int w = 0;
+        while (w + 1 < PAIR_WAVES && s_cc[w + 1] <= k) ++w;
+        const uint64_t wlo = (uint64_t)(blockIdx.x * PAIR_WAVES + w) * seg;
+        const FirstCont C = cont[wlo + (k - s_cc[w])];
+        const PairRes P = pres[C.i];
+        const EvLoc L = evloc[P.ev];
+        FirstState r{C.st, C.pos, C.last};
+        const int e = first_finish(pool, fdesc + 8 * P.p, text + L.ustart, (int)(L.uend - L.ustart), r);
+        if (e >= 0) {
+            pend[C.i] = e;
+            matched[wlo + atomicAdd(&s_mc[w], 1u)] = C.i;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < PAIR_WAVES) mcount[blockIdx.x * PAIR_WAVES + threadIdx.x] = s_mc[threadIdx.x];
 }
 
 // per matched pair: validator + hotword windows of the row's context variant -> likelihood
@@ -626,7 +751,8 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
                                                           const unsigned long long* __restrict__ pair_count,
                                                           uint64_t pair_cap, const uint32_t* __restrict__ matched,
                                                           const uint32_t* __restrict__ mcount, uint32_t nseg,
-                                                          const PairLoc* __restrict__ ploc,
+                                                          const EvLoc* __restrict__ evloc,
+                                                          const int32_t* __restrict__ pend,
                                                           PairRes* __restrict__ pres) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     const uint8_t* lb = load_image(img, li.total, lds4);
@@ -639,17 +765,29 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
     const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + li.off[EV_ROFF]);
     const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + li.off[EV_RIDS]);
     const uint8_t* text = text0 + offs[0];
-    const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg);
+    __shared__ uint32_t s_mp[PAIR_WAVES + 1];
+    const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg * PAIR_WAVES);
     for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
-        const uint32_t m = mcount[g];
-        const uint32_t* ms = matched + (uint64_t)g * seg;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int w = 0; w < PAIR_WAVES; ++w) {
+                s_mp[w] = run;
+                run += mcount[g * PAIR_WAVES + w];
+            }
+            s_mp[PAIR_WAVES] = run;
+        }
+        __syncthreads();
+        const uint32_t m = s_mp[PAIR_WAVES];
         for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) {
-            const uint32_t i = ms[k];
-            const PairLoc Lc = ploc[i];
+            int w = 0;
+            while (w + 1 < PAIR_WAVES && s_mp[w + 1] <= k) ++w;
+            const uint32_t i = matched[(uint64_t)(g * PAIR_WAVES + w) * seg + (k - s_mp[w])];
             const PairRes P = pres[i];
+            const EvLoc Lc = evloc[P.ev];
             const uint8_t* t0 = text + Lc.ustart;
             const int L = (int)(Lc.uend - Lc.ustart);
-            const int s = (int)(Lc.s - Lc.ustart), e = P.e;
+            const int s = (int)(Lc.s - Lc.ustart), e = pend[i];
             int lik = -1;
             if (validate(dval[P.p], t0 + s, e - s)) {
                 const uint32_t u = Lc.u;
@@ -686,11 +824,14 @@ constexpr int LIVE = 8;            // register-resident "previous match end" slo
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
                                                 const uint32_t* __restrict__ lane_np,
-                                                const PairLoc* __restrict__ ploc, const PairRes* __restrict__ pres,
+                                                const EvLoc* __restrict__ evloc, const PairRes* __restrict__ pres,
+                                                const int32_t* __restrict__ pend,
                                                 uint64_t pair_cap, const uint8_t* __restrict__ role,
                                                 const int16_t* __restrict__ ctx, pii_span* __restrict__ fd,
-                                                uint32_t* __restrict__ n_find, uint32_t* __restrict__ out_len) {
+                                                uint32_t* __restrict__ n_find, uint32_t* __restrict__ out_len,
+                                                const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    if (*err & ERR_QUEUE) return;           // the batch is re-run with a larger queue
     const uint8_t* lb = load_image(img, li.total, lds4);
     const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[SE_DTYPE]);
     const uint8_t* ven = lb + li.off[SE_VEN];
@@ -704,7 +845,7 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
     const uint32_t np = lane_np[c];
     if (np == 0 || lane_pair[c] + np > pair_cap) return;     // overflowed queue: the batch is re-run
     const PairRes* rl = pres + lane_pair[c];
-    const PairLoc* ll = ploc + lane_pair[c];
+    const int32_t* el = pend + lane_pair[c];
     const int T = R.T;
     // per-utterance state
     uint32_t u = 0xffffffffu;
@@ -747,22 +888,14 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
         }
     };
     for (uint32_t i0 = 0; i0 < np; i0 += 4) {
-        PairRes rr[4];
+        int32_t ee[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ee[j] = i0 + j < np ? el[i0 + j] : -1;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (i0 + j < np) {
-                rr[j] = rl[i0 + j];
-            } else {
-                rr[j].p = 0;
-                rr[j].lik = -1;
-                rr[j].e = -1;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const PairRes P = rr[j];
-            if (P.e < 0) continue;
-            const PairLoc Lc = ll[i0 + j];
+            if (ee[j] < 0) continue;
+            const PairRes P = rl[i0 + j];
+            const EvLoc Lc = evloc[P.ev];
             const int ps = (int)(Lc.s - Lc.ustart);
             if (Lc.u != u) {
                 if (u != 0xffffffffu) {
@@ -801,7 +934,7 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
                     if (lp[q] == p) prev_end = le[q];
             }
             if (s < prev_end) continue;               // inside p's previous match (finditer)
-            const int e = P.e;
+            const int e = ee[j];
             if (spilled) {
                 cur_s[p] = (uint32_t)e;
             } else {
@@ -963,13 +1096,15 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 
 __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t* __restrict__ span_offs,
                            uint32_t n_utt, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
-                           uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count) {
+                           uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count,
+                           const uint64_t* __restrict__ ev_count) {
     const uint64_t ob = out_offs[n_utt], ns = span_offs[n_utt];
     if (ob > out_cap || ns > span_cap) atomicOr(err, (uint32_t)ERR_CAPACITY);
     totals[0] = ob;
     totals[1] = ns;
     totals[2] = *err;
     totals[3] = *pair_count;
+    totals[4] = ev_count ? *ev_count : 0;
 }
 
 // ---------------------------------------------------------------------------------- k_redact
@@ -1013,7 +1148,7 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
                                                          const uint64_t* __restrict__ span_offs,
                                                          const uint32_t* __restrict__ err, uint8_t* __restrict__ out,
                                                          pii_span* __restrict__ spans,
-                                                         unsigned long long* __restrict__ hist) {
+                                                         uint32_t* __restrict__ hist_part) {
     __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (tile relative)
     __shared__ uint64_t s_psrc[PIECE_MAX + 1];     // piece source: text position, or bit 63 | token offset
     __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
@@ -1199,8 +1334,26 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
         }
     }
     __syncthreads();
-    for (int i = tid; i < R.T && i < 256; i += REDACT_BLOCK)
-        if (sh_hist[i]) atomicAdd(&hist[i], (unsigned long long)sh_hist[i]);
+    for (int i = tid; i < R.T && i < 256; i += REDACT_BLOCK) hist_part[(size_t)i * gridDim.x + blockIdx.x] = sh_hist[i];
+}
+
+// per-info-type totals of the redact tiles' histograms (one atomic per type, no same-address storms)
+__global__ __launch_bounds__(256) void k_hist_reduce(const uint32_t* __restrict__ hist_part, uint32_t n_tiles, int T,
+                                                     const uint32_t* __restrict__ err,
+                                                     unsigned long long* __restrict__ hist) {
+    __shared__ unsigned long long s_sum[4];
+    if (*err != 0) return;                   // k_redact did not run: the call is reported as failed
+    const int t = blockIdx.x;
+    unsigned long long v = 0;
+    for (uint32_t b = blockIdx.y * blockDim.x + threadIdx.x; b < n_tiles; b += gridDim.y * blockDim.x)
+        v += hist_part[(size_t)t * n_tiles + b];
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+        if (tot) atomicAdd(&hist[t], tot);
+    }
 }
 
 __global__ void k_noop() {}
@@ -1310,23 +1463,30 @@ struct pii_engine {
     uint32_t* stamp = nullptr;
     uint32_t epoch = 0;
     unsigned long long* hist = nullptr;
+    uint32_t* hist_part = nullptr;     // per redact tile, per info type
     // scratch
     uint64_t cap_bytes = 0;
     uint32_t cap_utt = 0;
+    size_t cap_bsum = 0;
     Event* ev = nullptr;
     pii_span* fd = nullptr;
     uint32_t *n_ev = nullptr, *n_find = nullptr, *out_len = nullptr, *incl = nullptr, *agg_f = nullptr;
     uint32_t* first_utt = nullptr;
     uint32_t* lane_cnt = nullptr;
     uint64_t* bnd = nullptr;
-    PairLoc* ploc = nullptr;
+    EvLoc* evloc = nullptr;
+    EvPairs* evpairs = nullptr;
+    uint64_t ev_cap = 0;
+    uint64_t* lane_ev = nullptr;      // exclusive scan of lane_cnt: first dense event index per lane
     PairRes* pres = nullptr;
+    int32_t* pend = nullptr;          // FIRST end per pair
     uint64_t pair_cap = 0;
     unsigned long long* pair_count = nullptr;
     uint64_t* lane_pair = nullptr;
     uint32_t* lane_np = nullptr;
     uint32_t* matched = nullptr;
-    uint32_t* mcount = nullptr;   // matched pairs per k_pair_first segment
+    uint32_t* mcount = nullptr;   // matched pairs per k_pair_first wavefront segment
+    FirstCont* cont = nullptr;
     uint32_t n_seg = 0;
     struct Call {
         const uint8_t* text;
@@ -1392,22 +1552,27 @@ int grow_pairs(pii_engine* e, uint64_t cap) {
         return PII_E_NOMEM;
     }
     int rc;
-    if ((rc = grow(e, e->ploc, cap)) || (rc = grow(e, e->pres, cap)) || (rc = grow(e, e->matched, cap))) return rc;
+    if ((rc = grow(e, e->pres, cap)) || (rc = grow(e, e->pend, cap)) || (rc = grow(e, e->matched, cap)) ||
+        (rc = grow(e, e->cont, cap)))
+        return rc;
     return PII_OK;
 }
 
 int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
     int rc = PII_OK;
+
     if (bytes > e->cap_bytes) {
         const uint64_t nb = std::max<uint64_t>(bytes + bytes / 8, 1 << 16);
         if ((rc = grow(e, e->ev, nb + 1))) return rc;
         if ((rc = grow(e, e->fd, nb / e->R.min_len + 2))) return rc;
         if ((rc = grow(e, e->first_utt, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->lane_cnt, nb / BYTES_PER_LANE + 2))) return rc;
+        if ((rc = grow(e, e->lane_ev, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->bnd, nb / 64 + 4))) return rc;
         if ((rc = grow(e, e->lane_pair, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->lane_np, nb / BYTES_PER_LANE + 2))) return rc;
         e->cap_bytes = nb;
+        e->cap_bsum = 0;
     }
     if (n_utt > e->cap_utt) {
         const uint32_t nu = std::max<uint32_t>(n_utt + n_utt / 8, 1024);
@@ -1423,8 +1588,14 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
         if ((rc = grow(e, e->agg_f, nblk))) return rc;
         if ((rc = grow(e, e->span_offs, (size_t)nu + 1))) return rc;
         if ((rc = grow(e, e->out_offs_tmp, (size_t)nu + 1))) return rc;
-        if ((rc = grow(e, e->bsum, (size_t)nu / SCAN_TILE + 2))) return rc;
+        if ((rc = grow(e, e->hist_part, ((size_t)nu / REDACT_UTT + 2) * (size_t)std::max(e->R.T, 1)))) return rc;
         e->cap_utt = nu;
+        e->cap_bsum = 0;
+    }
+    if (e->cap_bsum == 0) {   // scan block sums: the utterance scans and the per-lane pair-count scan
+        const size_t n = std::max<size_t>(e->cap_utt, e->cap_bytes / BYTES_PER_LANE + 2);
+        if ((rc = grow(e, e->bsum, n / SCAN_TILE + 2))) return rc;
+        e->cap_bsum = n;
     }
     return rc;
 }
@@ -1456,6 +1627,11 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         if ((rc = grow_pairs(e, cap))) return rc;
         e->pair_cap = cap;
     }
+    if (e->ev_cap < total_bytes / 16 + 4096) {
+        const uint64_t cap = total_bytes / 16 + 4096;
+        if ((rc = grow(e, e->evloc, cap)) || (rc = grow(e, e->evpairs, cap))) return rc;
+        e->ev_cap = cap;
+    }
     e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
                                ctx_info, st};
     const RulesDev& R = e->R;
@@ -1465,6 +1641,9 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
     HIPCHK(hipEventRecord(e->tev[0], st));
     const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
+    // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
+    const unsigned long long* pcount =
+        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, R.kw_always_min,
                                                                 e->first_utt, e->out_len, e->n_find, e->kw);
@@ -1472,9 +1651,16 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_bounds<<<(n_utt + 255) / 256, 256, 0, st>>>(offs, n_utt, (int64_t)((uintptr_t)text & 63), e->bnd);
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
                 R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->ev, e->lane_cnt);
-            k_pairs<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt,
-                                                           role, e->kw, e->ploc, e->pres, e->pair_cap, e->pair_count,
-                                                           e->lane_pair, e->lane_np, e->d_err);
+            const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
+            k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
+                                                        e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
+                                                        e->lane_pair, e->lane_ev, e->lane_np, e->d_err);
+            if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
+            if ((rc = exclusive_scan(e, e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
+            k_pairs<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
+                                                       e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
+                                                       e->lane_pair, e->lane_ev, e->lane_np, e->d_err);
+            k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
         }
         HIPCHK(hipGetLastError());
     }
@@ -1491,33 +1677,36 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipEventRecord(e->tev[2], st));
     if (n_utt > 0 && n_chunks > 0) {
         k_pair_first<<<e->n_seg, PAIR_BLOCK, e->img_first.li.total, st>>>(
-            e->img_first.d, e->img_first.li, text, offs, e->pair_count, e->pair_cap, e->ploc, e->pres, e->matched,
-            e->mcount);
+            e->img_first.d, e->img_first.li, text, offs, pcount, e->pair_cap, e->evloc, e->pres, e->pend, e->matched,
+            e->cont, e->mcount, e->d_err);
         k_pair_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
-            e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, e->pair_count, e->pair_cap, e->matched,
-            e->mcount, e->n_seg, e->ploc, e->pres);
+            e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
+            e->mcount, e->n_seg, e->evloc, e->pend, e->pres);
         k_select<<<(n_chunks + 255) / 256, 256, e->img_sel.li.total, st>>>(
-            R, e->img_sel.d, e->img_sel.li, n_chunks, e->lane_pair, e->lane_np, e->ploc, e->pres, e->pair_cap, role,
-            ctx, e->fd, e->n_find, e->out_len);
+            R, e->img_sel.d, e->img_sel.li, n_chunks, e->lane_pair, e->lane_np, e->evloc, e->pres, e->pend, e->pair_cap, role,
+            ctx, e->fd, e->n_find, e->out_len, e->d_err);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[3], st));
     if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
     if ((rc = exclusive_scan(e, e->n_find, n_utt, e->span_offs, st))) return rc;
     k_finalize<<<1, 1, 0, st>>>(out_offs, e->span_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
-                                e->pair_count);
+                                pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
-        if (n_chunks > 0)
-            k_redact<<<(n_utt + REDACT_UTT - 1) / REDACT_UTT, REDACT_BLOCK, 0, st>>>(
-                R, text, offs, n_utt, e->fd, e->n_find, out_offs, e->span_offs, e->d_err, out, spans, e->hist);
+        if (n_chunks > 0) {
+            const uint32_t n_tiles = (n_utt + REDACT_UTT - 1) / REDACT_UTT;
+            k_redact<<<n_tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, n_utt, e->fd, e->n_find, out_offs,
+                                                       e->span_offs, e->d_err, out, spans, e->hist_part);
+            k_hist_reduce<<<dim3(std::min(R.T, 256), std::max(1u, std::min(32u, n_tiles / 256))), 256, 0, st>>>(e->hist_part, n_tiles, R.T, e->d_err, e->hist);
+        }
         k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
                                                           e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
-    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(e->tev[6], st));
     return PII_OK;
 }
@@ -1571,7 +1760,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         return PII_E_RULES;
     };
     if (R.P > P_MAX) return fail("more detector patterns than P_MAX");
-    if ((int64_t)R.SD * R.CD >= 32768 || (int64_t)R.SK * R.CK >= 32768) return fail("SCAN tables exceed 15-bit rows");
+    // scan table entries are 16-bit LDS byte addresses (k_scan layout: class map, D rows, K rows)
+    const uint32_t td_words = (uint32_t)((R.SD * R.CD + 1) / 2), tk_words = (uint32_t)((R.SK * R.CK + 1) / 2);
+    const uint32_t tk_base = SCAN_TD_BASE + td_words * 4;
+    if ((uint64_t)tk_base + (uint64_t)tk_words * 4 > 65536) return fail("SCAN tables exceed 64 KiB of LDS");
     if (R.T > 65535) return fail("too many types");
     // names + tokens
     {
@@ -1594,9 +1786,18 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     std::vector<uint16_t> td(R.SD * R.CD), tk(R.SK * R.CK);
     {
         const uint16_t* s = reinterpret_cast<const uint16_t*>(find("scan.d.trans")->data);
-        for (int i = 0; i < R.SD * R.CD; ++i) td[i] = (uint16_t)(((s[i] & 0x7fff) * R.CD) | (s[i] & 0x8000));
+        for (int i = 0; i < R.SD * R.CD; ++i)
+            td[i] = (uint16_t)((SCAN_TD_BASE + (s[i] & 0x7fff) * R.CD * 2) | (s[i] >> 15));
         const uint16_t* k = reinterpret_cast<const uint16_t*>(find("scan.k.trans")->data);
-        for (int i = 0; i < R.SK * R.CK; ++i) tk[i] = (uint16_t)(((k[i] & 0x7fff) * R.CK) | (k[i] & 0x8000));
+        for (int i = 0; i < R.SK * R.CK; ++i)
+            tk[i] = (uint16_t)((tk_base + (k[i] & 0x7fff) * R.CK * 2) | (k[i] >> 15));
+    }
+    R.d_start = (int)(SCAN_TD_BASE + R.d_start * R.CD * 2);     // start rows as LDS byte addresses
+    R.k_start = (int)(tk_base + R.k_start * R.CK * 2);
+    std::vector<uint32_t> cmap4(256);
+    {
+        const uint16_t* c2 = reinterpret_cast<const uint16_t*>(find("scan.cmap2")->data);
+        for (int b = 0; b < 256; ++b) cmap4[b] = 2u * (c2[b] & 0xffu) | (2u * (uint32_t)(c2[b] >> 8)) << 16;
     }
     std::vector<uint16_t> k_acc_min;
     {
@@ -1604,6 +1805,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         const uint32_t* off = reinterpret_cast<const uint32_t*>(so->data);
         const uint16_t* ids = reinterpret_cast<const uint16_t*>(find("scan.k.acc_ids")->data);
         const size_t nsets = so->bytes / 4 - 1;
+        R.n_kacc = (uint32_t)nsets;
+        R.n_dacc = (uint32_t)(find("scan.d.acc_off")->bytes / 4 - 1);
         for (size_t a = 0; a < nsets; ++a) {
             int m = KW_NONE;
             for (uint32_t i = off[a]; i < off[a + 1]; ++i) m = std::min<int>(m, ids[i]);
@@ -1649,7 +1852,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         return puts.size() - 1;
     };
     auto addsec = [&](const char* nm) { return add(find(nm)->data, find(nm)->bytes); };
-    size_t i_cmap = addsec("scan.cmap2"), i_td = add(td.data(), td.size() * 2), i_tk = add(tk.data(), tk.size() * 2);
+    size_t i_cmap = add(cmap4.data(), cmap4.size() * 4), i_td = add(td.data(), td.size() * 2), i_tk = add(tk.data(), tk.size() * 2);
     size_t i_dacc = addsec("scan.d.accid"), i_doff = addsec("scan.d.acc_off"), i_dids = addsec("scan.d.acc_ids");
     size_t i_kacc = addsec("scan.k.accid"), i_kmin = add(k_acc_min.data(), k_acc_min.size() * 2);
     size_t i_dt = addsec("det.type"), i_dv = addsec("det.validator"), i_dl = addsec("det.lik"),
@@ -1665,7 +1868,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     if (hipMemcpy(e->d_rules, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) return fail("upload failed");
     uint8_t* b = static_cast<uint8_t*>(e->d_rules);
     auto at = [&](size_t i) { return b + puts[i].off; };
-    R.cmap2 = (const uint16_t*)at(i_cmap);
+    R.cmap4 = (const uint32_t*)at(i_cmap);
     R.td = (const uint16_t*)at(i_td);
     R.tk = (const uint16_t*)at(i_tk);
     R.d_accid = (const uint16_t*)at(i_dacc);
@@ -1736,9 +1939,9 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             e->n_cu = prop.multiProcessorCount;
         e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
-        if (hipMalloc(&e->mcount, e->n_seg * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
+        if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
-    e->scan_lds = 512 + (size_t)((R.SD * R.CD + 1) / 2) * 4 + (size_t)((R.SK * R.CK + 1) / 2) * 4;
+    e->scan_lds = 1024 + (size_t)((R.SD * R.CD + 1) / 2) * 4 + (size_t)((R.SK * R.CK + 1) / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     if (e->scan_lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess)
@@ -1769,7 +1972,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->ploc, e->pres, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx};
@@ -1835,10 +2038,16 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
     for (int attempt = 0; (e->h_totals[2] & ERR_QUEUE) && attempt < 4; ++attempt) {
         // the (start, pattern) pair queue overflowed: grow it to the exact need and run the batch again
         // (the conversation context was not committed, so the re-run is idempotent)
-        const uint64_t need = e->h_totals[3] + 4096;
-        int rc = grow_pairs(e, need);
+        const uint64_t need = e->h_totals[3] + 4096, need_ev = e->h_totals[4] + 4096;
+        if (need_ev > e->ev_cap) {
+            int rc = grow(e, e->evloc, need_ev);
+            if (!rc) rc = grow(e, e->evpairs, need_ev);
+            if (rc) return rc;
+            e->ev_cap = need_ev;
+        }
+        int rc = grow_pairs(e, std::max(need, e->pair_cap));
         if (rc) return rc;
-        e->pair_cap = need;
+        e->pair_cap = std::max(need, e->pair_cap);
         const pii_engine::Call c = e->last;
         e->epoch += 0;
         rc = run_pipeline(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
