@@ -28,6 +28,8 @@ synth = importlib.import_module("context-based-pii_amd.synth")
 compiler = importlib.import_module("context-based-pii_amd.compiler")
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy ceiling
+LANE_BYTES = 1024        # BYTES_PER_LANE of csrc/pii_engine.hip (k_scan lane = utterances starting in 1 KiB)
+SOURCES = ["context-based-pii_amd/csrc/pii_engine.hip", "context-based-pii_amd/csrc/pii_device.h"]
 METRIC = "transcript MB/s scanned+redacted per node (1/2/4/8 GPU) and % HBM roofline"
 
 # --------------------------------------------------------------------------- CPU baseline (oracle)
@@ -73,6 +75,28 @@ def cpu_baseline(bank, seconds: float = 15.0):
                       f"distribution, oracle/pii_oracle.py process_rows, multiprocessing fork pool, wall {wall:.1f}s"}
 
 
+def source_digest() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES:
+        h.update(open(os.path.join(ROOT, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(kernel: str, n_bytes: int):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (tools/pmc_traffic.py), but only
+    when they were measured on exactly these kernel sources and this workload size; else None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    k = t.get("kernels", {}).get(kernel)
+    if not k or t.get("source_digest") != source_digest() or t.get("bytes_per_gpu") != n_bytes:
+        return None
+    return k.get("hbm_bytes")
+
+
 # --------------------------------------------------------------------------- GPU corpus assembly
 def gpu_corpus(meta, bank, dev):
     import torch
@@ -112,7 +136,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     bank = synth.build_bank(16384, 16384, seed=synth.SEED)
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(bank, args.cpu_seconds)          # before any HIP initialisation (fork pool)
 
     import torch
@@ -164,11 +188,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    per_kernel = np.zeros(6)
+    per_stage = np.zeros(6)
+    k_ms = {"k_scan": 0.0, "k_redact": 0.0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ob, ns = step()
-        per_kernel += np.array(eng.timings())
+        per_stage += np.array(eng.timings())
+        for k, v in eng.kernel_timings().items():
+            k_ms[k] += v
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,18 +204,25 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    per_kernel /= args.steps
+    per_stage /= args.steps
+    k_ms = {k: v / args.steps for k, v in k_ms.items()}
+    n_pairs, n_events = eng.queue_sizes()
+    n_lanes = (n_bytes + LANE_BYTES - 1) // LANE_BYTES
     ms_step = elapsed / args.steps * 1e3
     total_bytes = n_bytes * world * args.steps
     mbps = total_bytes / elapsed / 1e6
-    # algorithmic bytes: in + out + in/out offsets + slot/role + spans
+    # SURVEY 8(d) whole-path algorithmic bytes: in + out + in/out offsets + slot/role + spans
     B = n_bytes + ob + 8 * (n + 1) * 2 + 5 * n + 16 * ns
-    t_pipe = per_kernel[5] / 1e3
-    # dominant kernel: the reverse DFA scan; algorithmic bytes per launch = utterance bytes read +
-    # 8(U+1) offsets + U roles + U*(4+2) per-row event count / context results written
-    scan_B = n_bytes + 8 * (n + 1) + n + 6 * n
-    t_scan = per_kernel[0] / 1e3
-    scan_GBps = scan_B / t_scan / 1e9
+    t_pipe = per_stage[5] / 1e3
+    # dominant kernel k_scan, algorithmic bytes per launch (DESIGN.md "Roofline accounting"):
+    # every utterance byte once + the utterance-start bitmap (1 bit per byte) + per lane its
+    # first_utt pair, offsets pair, event count (24 B) + 8 B per event written
+    scan_B = n_bytes + (n_bytes + 63) // 64 * 8 + 24 * n_lanes + 8 * n_events
+    scan_GBps = scan_B / (k_ms["k_scan"] / 1e3) / 1e9
+    # k_redact: input + output bytes, its offset/count reads, the span copy (read + write)
+    red_B = n_bytes + ob + 8 * (n + 1) * 3 + 4 * n + 32 * ns
+    red_GBps = red_B / (k_ms["k_redact"] / 1e3) / 1e9
+    traffic = measured_traffic("k_scan", n_bytes)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
@@ -200,12 +234,18 @@ def main():
                        "rules": "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
             "utt_per_s": round(n * world * args.steps / elapsed, 1),
             "spans_per_step_per_gpu": ns,
-            "kernels_ms": {k: round(float(v), 4) for k, v in zip(
-                ["scan", "context", "resolve", "offsets", "redact", "pipeline"], per_kernel)},
+            "queues_per_step_per_gpu": {"scan_events": n_events, "candidate_pairs": n_pairs},
+            "stages_ms": {k: round(float(v), 4) for k, v in zip(
+                ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
+            "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
             "pipeline": {"algorithmic_bytes": int(B), "GBps": round(B / t_pipe / 1e9, 1),
                          "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
             "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": None},
+                         "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "algorithmic_bytes": int(scan_B), "launch_ms": round(k_ms["k_scan"], 4)},
+            "roofline_redact": {"bound": "hbm", "kernel": "k_redact", "achieved": round(red_GBps, 1),
+                                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(red_GBps / HBM_PEAK_GBPS, 4),
+                                "algorithmic_bytes": int(red_B), "launch_ms": round(k_ms["k_redact"], 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

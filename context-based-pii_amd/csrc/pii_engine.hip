@@ -7,7 +7,7 @@
 // Pipeline per batch (one HIP stream, no host round trip until pii_sync):
 //   k_chunk_index  lane -> utterance ranges of ~BYTES_PER_LANE bytes (load balance, no halo needed);
 //                  per-row defaults
-//   k_bounds       utterance-start bitmap aligned with the scan's 64-byte blocks
+//   k_lane_bits    utterance-start words per lane and 64-byte block (lane-interleaved, coalesced)
 //   k_scan         REVERSE two-automaton DFA scan, tables in LDS.  D = relaxed detector prefilter,
 //                  K = exact context keywords.  Emits candidate STARTS (events) per lane
 //   k_pairs        agent-row context group (extract_expected_pii, main.py:558-578); (start, pattern)
@@ -43,6 +43,7 @@ constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
 constexpr uint32_t BYTES_PER_LANE = 1024;
 constexpr int KW_NONE = 0x7fff;
+constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
 enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8 };
 
@@ -123,43 +124,86 @@ __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
     return (x >> ((K & 3) * 8)) & 0xffu;
 }
 
-// Utterance-start bitmap: bit k of word w <=> a non-empty utterance starts at text position
-// 64*w - mis + k - (word 0 offset), where mis = (text address) & 63, i.e. the bitmap words line up with
-// the scan's aligned 64-byte blocks; the batch end carries a bit too.  The owner of a word (the first
-// utterance starting in it) writes it and zero-fills the words up to the next owner, so every word is
-// written exactly once.
-__global__ void k_bounds(const uint64_t* __restrict__ offs, uint32_t n_utt, int64_t mis,
-                         uint64_t* __restrict__ bnd) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n_utt) return;
-    const int64_t w0 = ((int64_t)offs[0] + mis) >> 6;
-    const int64_t wu = ((int64_t)offs[u] + mis) >> 6;
-    if (u > 0 && (((int64_t)offs[u - 1] + mis) >> 6) == wu) return;      // not the owner
+// Utterance-start words, lane-interleaved: word[i * n_lanes + c] holds, for lane c's i-th block from
+// the top (aligned 64-byte block b_hi(c) - i, b = (position + mis) >> 6, mis = text address & 63),
+// bit k <=> a non-empty utterance starts at position 64b - mis + k; the lane's top block also carries
+// the bit of the position after its range (the next lane's first start / the batch end), which
+// resets the automata before the lane's last byte.  All lanes of a wavefront read word i at the same
+// iteration, so the scan's word loads are coalesced.  Blocks past LANE_WORDS use a slow path.
+constexpr int LANE_WORDS = 32;
+
+__device__ __forceinline__ void lane_range(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
+                                           uint32_t c, uint32_t& u0, uint32_t& u1, int64_t& lo, int64_t& hi) {
+    u0 = first_utt[c];
+    u1 = first_utt[c + 1];
+    lo = (int64_t)offs[u0];
+    hi = (int64_t)offs[u1] - 1;
+}
+
+// bits of lane c's i-th block from the top (the slow path for i >= LANE_WORDS: binary search + walk
+// over offs; everything is re-derived from (c, i) so the scan keeps nothing live for it)
+__device__ __attribute__((noinline)) uint64_t block_bits_slow(const uint64_t* __restrict__ offs,
+                                                              const uint32_t* __restrict__ first_utt, uint32_t c,
+                                                              uint32_t i, int64_t mis) {
+    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
+    const int64_t b_hi = ((int64_t)offs[u1] - 1 + mis) >> 6;
+    const int64_t blk = b_hi - i;
+    const int64_t plo = blk * 64 - mis, phi = plo + 64;       // positions [plo, phi)
+    // largest u in [u0, u1] with offs[u] < phi
+    uint32_t a = u0, b = u1;
+    while (a < b) {
+        const uint32_t m = (a + b + 1) >> 1;
+        if ((int64_t)offs[m] < phi) a = m;
+        else b = m - 1;
+    }
     uint64_t bits = 0;
-    uint32_t v = u;
-    for (;; ++v) {
-        if (v == n_utt) {
-            // batch end: its bit goes in its own word (this one or one past the zero-filled gap)
-            const int64_t se = (int64_t)offs[n_utt];
-            const int64_t we = (se + mis) >> 6;
-            if (we == wu) {
-                bits |= 1ull << ((se + mis) & 63);
-                bnd[wu - w0] = bits;
-            } else {
-                bnd[wu - w0] = bits;
-                for (int64_t w = wu + 1; w < we; ++w) bnd[w - w0] = 0;
-                bnd[we - w0] = 1ull << ((se + mis) & 63);
+    for (int64_t u = a; u >= (int64_t)u0; --u) {
+        const int64_t su = (int64_t)offs[u];
+        if (su < plo) break;
+        const bool reset = u == (int64_t)u1;                   // the position after the lane's range
+        if ((reset && blk == b_hi) || (!reset && (int64_t)offs[u + 1] > su)) bits |= 1ull << (su - plo);
+    }
+    return bits;
+}
+
+// one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
+__global__ __launch_bounds__(256) void k_lane_bits(const uint64_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+                                                   int64_t mis, uint64_t* __restrict__ words) {
+    __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t cw0 = c - lane;
+    const uint32_t cw1 = min(cw0 + 64, n_chunks);
+    const uint32_t U0 = cw0 < n_chunks ? first_utt[cw0] : 0u;
+    const uint32_t U1 = cw0 < n_chunks ? first_utt[cw1] : 0u;
+    const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
+    int64_t* so = s_off[wv];
+    if (staged && cw0 < n_chunks)
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (int64_t)offs[U0 + k];
+    __syncthreads();
+    if (c >= n_chunks) return;
+    auto uoff = [&](int64_t u) { return staged ? so[u - U0] : (int64_t)offs[u]; };
+    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
+    const int64_t lo = uoff(u0), hi = uoff(u1) - 1;
+    if (hi < lo) return;
+    const int64_t b_hi = (hi + mis) >> 6, b_lo = (lo + mis) >> 6;
+    const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
+    int64_t u = u1;
+    int64_t su = uoff(u);
+    for (int64_t i = 0; i < nw; ++i) {
+        const int64_t blk = b_hi - i;
+        const int64_t plo = blk * 64 - mis;
+        uint64_t bits = 0;
+        while (u >= (int64_t)u0 && su >= plo) {
+            if (su < plo + 64) {
+                const bool reset = u == (int64_t)u1;
+                if ((reset && i == 0) || (!reset && uoff(u + 1) > su)) bits |= 1ull << (su - plo);
             }
-            return;
+            --u;
+            if (u >= (int64_t)u0) su = uoff(u);
         }
-        const int64_t sv = (int64_t)offs[v];
-        const int64_t wv = (sv + mis) >> 6;
-        if (wv != wu) {
-            bnd[wu - w0] = bits;
-            for (int64_t w = wu + 1; w < wv; ++w) bnd[w - w0] = 0;
-            return;
-        }
-        if ((int64_t)offs[v + 1] > sv) bits |= 1ull << ((sv + mis) & 63);
+        words[(uint64_t)i * n_chunks + c] = bits;
     }
 }
 
@@ -171,78 +215,74 @@ __device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
     return *reinterpret_cast<lds_u16_t*>((size_t)addr);
 }
 
-__device__ __forceinline__ void scan_emit(Event* __restrict__ evl, uint32_t& cnt, int64_t pos, int64_t lo_r,
-                                          int64_t hi_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
-    if (pos >= lo_r && pos <= hi_r) {
+// the lane's events go to ev[lo_r ...] (its own arena: a lane never has more events than bytes + 1)
+__device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt, uint32_t pos, uint32_t lo_r,
+                                          uint32_t len_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
+    if (pos - lo_r <= len_r) {
         Event e;
         e.pos = (uint32_t)pos;
         e.sd = (uint16_t)((ad - SCAN_TD_BASE) >> 1);     // transition index (row * CD + class)
         e.sk = (uint16_t)((ak - tk_base) >> 1);
-        evl[cnt++] = e;
+        ev[(uint64_t)lo_r + cnt++] = e;
     }
 }
 
 // utterance start at pos: the end-of-text pseudo step, then reset
 __device__ __forceinline__ void scan_bot(const uint8_t* lds, uint32_t eot_d, uint32_t eot_k, uint32_t d_start,
                                          uint32_t k_start, uint32_t tk_base, uint32_t& sd, uint32_t& sk,
-                                         uint32_t& cnt, Event* __restrict__ evl, int64_t pos, int64_t lo_r,
-                                         int64_t hi_r) {
+                                         uint32_t& cnt, Event* __restrict__ ev, uint32_t pos, uint32_t lo_r,
+                                         uint32_t len_r) {
     (void)lds;
     const uint32_t nd = lds_u16(sd + eot_d);
     const uint32_t nk = lds_u16(sk + eot_k);
-    if ((nd | nk) & 1u) scan_emit(evl, cnt, pos, lo_r, hi_r, sd + eot_d, sk + eot_k, tk_base);
+    if ((nd | nk) & 1u) scan_emit(ev, cnt, pos, lo_r, len_r, sd + eot_d, sk + eot_k, tk_base);
     sd = d_start;
     sk = k_start;
 }
 
-#define SCAN_STEP(K, OFF)                                                                         \
+// byte classes of 8 bytes (HALF = 0: bytes 8..15 of the chunk, 1: bytes 0..7), issued together
+#define SCAN_CLASSES8(W, H)                                                                       \
+    cc[0] = s_cmap[byte_c<(H) + 0>(W)];                                                           \
+    cc[1] = s_cmap[byte_c<(H) + 1>(W)];                                                           \
+    cc[2] = s_cmap[byte_c<(H) + 2>(W)];                                                           \
+    cc[3] = s_cmap[byte_c<(H) + 3>(W)];                                                           \
+    cc[4] = s_cmap[byte_c<(H) + 4>(W)];                                                           \
+    cc[5] = s_cmap[byte_c<(H) + 5>(W)];                                                           \
+    cc[6] = s_cmap[byte_c<(H) + 6>(W)];                                                           \
+    cc[7] = s_cmap[byte_c<(H) + 7>(W)];
+
+// SCAN_STEP reads cc[K] for K in 0..15; with 8 classes in flight it is invoked with K - H
+#define SCAN_STEP8(J, H, OFF)                                                                     \
     {                                                                                             \
-        const uint32_t ad = sd + (cc[K] & 0xffffu);                                               \
-        const uint32_t ak = sk + (cc[K] >> 16);                                                   \
+        const uint32_t ad = sd + (cc[J] & 0xffffu);                                               \
+        const uint32_t ak = sk + (cc[J] >> 16);                                                   \
         const uint32_t nd = lds_u16(ad);                                                          \
         const uint32_t nk = lds_u16(ak);                                                          \
         sd = nd & 0xfffeu;                                                                        \
         sk = nk & 0xfffeu;                                                                        \
-        if (__builtin_expect((((nd | nk) & 1u) | (b16 & (1u << (K)))) != 0, 0)) {                 \
-            if ((nd | nk) & 1u) scan_emit(evl, cnt, bpos + (OFF) + (K) + 1, lo_r, hi_r, ad, ak, tk_base); \
-            if (b16 & (1u << (K)))                                                                \
-                scan_bot(lds, eot_d, eot_k, d_start, k_start, tk_base, sd, sk, cnt, evl, bpos + (OFF) + (K), lo_r, hi_r); \
+        if (__builtin_expect((((nd | nk) & 1u) | (b16 & (1u << ((H) + (J))))) != 0, 0)) {         \
+            if ((nd | nk) & 1u) scan_emit(ev, cnt, bpos + (OFF) + (H) + (J) + 1, lo_r, len_r, ad, ak, tk_base); \
+            if (b16 & (1u << ((H) + (J))))                                                        \
+                scan_bot(lds, eot_d, eot_k, d_start, k_start, tk_base, sd, sk, cnt, ev, bpos + (OFF) + (H) + (J), lo_r, len_r); \
         }                                                                                         \
     }
 
-#define SCAN_CLASSES(W)                                                                           \
-    cc[0] = s_cmap[byte_c<0>(W)];                                                                 \
-    cc[1] = s_cmap[byte_c<1>(W)];                                                                 \
-    cc[2] = s_cmap[byte_c<2>(W)];                                                                 \
-    cc[3] = s_cmap[byte_c<3>(W)];                                                                 \
-    cc[4] = s_cmap[byte_c<4>(W)];                                                                 \
-    cc[5] = s_cmap[byte_c<5>(W)];                                                                 \
-    cc[6] = s_cmap[byte_c<6>(W)];                                                                 \
-    cc[7] = s_cmap[byte_c<7>(W)];                                                                 \
-    cc[8] = s_cmap[byte_c<8>(W)];                                                                 \
-    cc[9] = s_cmap[byte_c<9>(W)];                                                                 \
-    cc[10] = s_cmap[byte_c<10>(W)];                                                               \
-    cc[11] = s_cmap[byte_c<11>(W)];                                                               \
-    cc[12] = s_cmap[byte_c<12>(W)];                                                               \
-    cc[13] = s_cmap[byte_c<13>(W)];                                                               \
-    cc[14] = s_cmap[byte_c<14>(W)];                                                               \
-    cc[15] = s_cmap[byte_c<15>(W)];
-
 #define SCAN_SUB(W, OFF)                                                                          \
     {                                                                                             \
-        uint32_t cc[16];                                                                          \
-        SCAN_CLASSES(W)                                                                           \
+        uint32_t cc[8];                                                                           \
         const uint32_t b16 = (uint32_t)(bits >> (OFF)) & 0xffffu;                                 \
-        SCAN_STEP(15, OFF) SCAN_STEP(14, OFF) SCAN_STEP(13, OFF) SCAN_STEP(12, OFF)               \
-        SCAN_STEP(11, OFF) SCAN_STEP(10, OFF) SCAN_STEP(9, OFF) SCAN_STEP(8, OFF)                 \
-        SCAN_STEP(7, OFF) SCAN_STEP(6, OFF) SCAN_STEP(5, OFF) SCAN_STEP(4, OFF)                   \
-        SCAN_STEP(3, OFF) SCAN_STEP(2, OFF) SCAN_STEP(1, OFF) SCAN_STEP(0, OFF)                   \
+        SCAN_CLASSES8(W, 8)                                                                       \
+        SCAN_STEP8(7, 8, OFF) SCAN_STEP8(6, 8, OFF) SCAN_STEP8(5, 8, OFF) SCAN_STEP8(4, 8, OFF)   \
+        SCAN_STEP8(3, 8, OFF) SCAN_STEP8(2, 8, OFF) SCAN_STEP8(1, 8, OFF) SCAN_STEP8(0, 8, OFF)   \
+        SCAN_CLASSES8(W, 0)                                                                       \
+        SCAN_STEP8(7, 0, OFF) SCAN_STEP8(6, 0, OFF) SCAN_STEP8(5, 0, OFF) SCAN_STEP8(4, 0, OFF)   \
+        SCAN_STEP8(3, 0, OFF) SCAN_STEP8(2, 0, OFF) SCAN_STEP8(1, 0, OFF) SCAN_STEP8(0, 0, OFF)   \
     }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ offs, uint32_t n_utt,
                                                      const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                     const uint64_t* __restrict__ bnd, Event* __restrict__ ev,
+                                                     const uint64_t* __restrict__ words, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
@@ -263,53 +303,57 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
-    const int64_t base = (int64_t)offs[0];
-    const int64_t lo = (int64_t)offs[u0];   // lane range [lo, hi]
-    const int64_t hi = (int64_t)offs[u1] - 1;
-    const int64_t end = (int64_t)offs[n_utt];
+    const uint64_t base = offs[0];
+    // positions relative to the batch base fit 32 bits (PII_MAX_BATCH_BYTES); 32-bit arithmetic keeps
+    // the lane's bookkeeping small (VGPRs decide this kernel's occupancy)
+    const uint32_t lo_r = (uint32_t)(offs[u0] - base);      // lane range [lo_r, hi_r]
+    const uint32_t hi_r = (uint32_t)(offs[u1] - base) - 1u;
+    const uint32_t end_r = (uint32_t)(offs[n_utt] - base);
     uint32_t cnt = 0;
-    if (hi >= lo) {
-        Event* __restrict__ evl = ev + (lo - base);
-        const int64_t lo_r = lo - base, hi_r = hi - base;
+    if (offs[u1] > offs[u0]) {
+        const uint32_t len_r = hi_r - lo_r;
         const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
         const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
         uint32_t sd = d_start, sk = k_start;
-        // aligned 64-byte blocks in ADDRESS space: block b covers positions [64b - mis, 64b - mis + 64)
-        const int64_t mis = (int64_t)((uintptr_t)text & 63);
-        const uint4* __restrict__ tp = reinterpret_cast<const uint4*>(text - mis);
-        const int64_t b0 = (base + mis) >> 6;
-        const int64_t b_hi = (hi + mis) >> 6;
-        const int64_t b_lo = (lo + mis) >> 6;
+        // aligned 64-byte blocks of the ADDRESS space, numbered from the one holding the batch base:
+        // block bb covers relative positions [64 bb - r0, 64 bb - r0 + 64)
+        const uintptr_t abase = (uintptr_t)(text + base);
+        const uint32_t r0 = (uint32_t)(abase & 63);
+        const uint4* __restrict__ tpb = reinterpret_cast<const uint4*>(abase - r0);
+        const uint32_t bb_hi = (hi_r + r0) >> 6, bb_lo = (lo_r + r0) >> 6;
         // the top block: only chunks holding a batch byte are read (the rest step as zero bytes
         // before the end-of-batch / next-utterance reset)
-        const int64_t q_end = (end - 1 + mis) >> 4;               // last chunk with a batch byte
-        uint4 n0 = tp[4 * b_hi], n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
-        if (4 * b_hi + 1 <= q_end) n1 = tp[4 * b_hi + 1];
-        if (4 * b_hi + 2 <= q_end) n2 = tp[4 * b_hi + 2];
-        if (4 * b_hi + 3 <= q_end) n3 = tp[4 * b_hi + 3];
-        uint64_t nb = bnd[b_hi - b0];
-        for (int64_t blk = b_hi; blk >= b_lo; --blk) {
+        const uint32_t q_end = (end_r - 1 + r0) >> 4;               // last chunk with a batch byte
+        uint4 n0 = tpb[4 * bb_hi], n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
+        if (4 * bb_hi + 1 <= q_end) n1 = tpb[4 * bb_hi + 1];
+        if (4 * bb_hi + 2 <= q_end) n2 = tpb[4 * bb_hi + 2];
+        if (4 * bb_hi + 3 <= q_end) n3 = tpb[4 * bb_hi + 3];
+        uint64_t nb = words[c];
+        for (uint32_t bb = bb_hi;; --bb) {
             const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
             const uint64_t bits = nb;
-            if (blk > b_lo) {
-                const int64_t q = 4 * (blk - 1);
-                n0 = tp[q];
-                n1 = tp[q + 1];
-                n2 = tp[q + 2];
-                n3 = tp[q + 3];
-                nb = bnd[blk - 1 - b0];
+            if (bb > bb_lo) {
+                const uint4* q = tpb + 4 * (bb - 1);
+                n0 = q[0];
+                n1 = q[1];
+                n2 = q[2];
+                n3 = q[3];
+                const uint32_t i = bb_hi - (bb - 1);
+                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * n_chunks + c]
+                                              : block_bits_slow(offs, first_utt, c, i, (int64_t)((uintptr_t)text & 63));
             }
-            const int64_t bpos = blk * 64 - mis - base;        // position of the block's byte 0
+            const uint32_t bpos = 64u * bb - r0;        // relative position of the block's byte 0 (mod 2^32)
             SCAN_SUB(w3, 48)
             SCAN_SUB(w2, 32)
             SCAN_SUB(w1, 16)
             SCAN_SUB(w0, 0)
+            if (bb == bb_lo) break;
         }
     }
     lane_cnt[c] = cnt;
 }
-#undef SCAN_STEP
-#undef SCAN_CLASSES
+#undef SCAN_STEP8
+#undef SCAN_CLASSES8
 #undef SCAN_SUB
 
 // ---------------------------------------------------------------------------- context (a11)
@@ -495,7 +539,6 @@ struct FirstCont {     // a FIRST run still alive after its first window
 // instead of issuing dependent, uncoalesced global loads.  A wavefront whose lanes cover more than
 // PAIRS_UCAP utterances (very short rows) walks global memory instead.
 constexpr int PAIRS_BLOCK = 256;
-constexpr int PAIRS_UCAP = 1024;
 
 // Two launches: WRITE = false counts each lane's pairs (and records the AGENT rows' keyword groups),
 // an exclusive scan of the counts gives every lane its block of the queue (lane order, no atomics),
@@ -1521,6 +1564,9 @@ struct pii_engine {
     int16_t* h_ctx = nullptr;
     hipEvent_t tev[7] = {};
     float last_ms[6] = {};
+    hipEvent_t kev[4] = {};           // around k_scan and k_redact (the roofline kernels)
+    bool kev_valid = false;
+    float last_kms[2] = {};
 };
 
 #define HIPCHK(x)                                                                  \
@@ -1568,7 +1614,7 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
         if ((rc = grow(e, e->first_utt, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->lane_cnt, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->lane_ev, nb / BYTES_PER_LANE + 2))) return rc;
-        if ((rc = grow(e, e->bnd, nb / 64 + 4))) return rc;
+        if ((rc = grow(e, e->bnd, (nb / BYTES_PER_LANE + 2) * LANE_WORDS))) return rc;
         if ((rc = grow(e, e->lane_pair, nb / BYTES_PER_LANE + 2))) return rc;
         if ((rc = grow(e, e->lane_np, nb / BYTES_PER_LANE + 2))) return rc;
         e->cap_bytes = nb;
@@ -1639,6 +1685,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     e->epoch += 1;
     HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), st));
     HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
+    e->kev_valid = n_utt > 0 && total_bytes > 0;
     HIPCHK(hipEventRecord(e->tev[0], st));
     const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
     // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
@@ -1648,9 +1695,12 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, R.kw_always_min,
                                                                 e->first_utt, e->out_len, e->n_find, e->kw);
         if (n_chunks > 0) {
-            k_bounds<<<(n_utt + 255) / 256, 256, 0, st>>>(offs, n_utt, (int64_t)((uintptr_t)text & 63), e->bnd);
+            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(offs, e->first_utt, n_chunks,
+                                                                (int64_t)((uintptr_t)text & 63), e->bnd);
+            HIPCHK(hipEventRecord(e->kev[0], st));
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
                 R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->ev, e->lane_cnt);
+            HIPCHK(hipEventRecord(e->kev[1], st));
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
             k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
                                                         e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
@@ -1697,8 +1747,10 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     if (n_utt > 0) {
         if (n_chunks > 0) {
             const uint32_t n_tiles = (n_utt + REDACT_UTT - 1) / REDACT_UTT;
+            HIPCHK(hipEventRecord(e->kev[2], st));
             k_redact<<<n_tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, n_utt, e->fd, e->n_find, out_offs,
                                                        e->span_offs, e->d_err, out, spans, e->hist_part);
+            HIPCHK(hipEventRecord(e->kev[3], st));
             k_hist_reduce<<<dim3(std::min(R.T, 256), std::max(1u, std::min(32u, n_tiles / 256))), 256, 0, st>>>(e->hist_part, n_tiles, R.T, e->d_err, e->hist);
         }
         k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
@@ -1948,6 +2000,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         return fail("cannot raise LDS limit");
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     e->own_stream = true;
+    for (auto& t : e->kev)
+        if (hipEventCreate(&t) != hipSuccess) return fail("event");
     for (auto& t : e->tev)
         if (hipEventCreate(&t) != hipSuccess) return fail("event");
     const size_t ns = std::max<uint32_t>(1, n_conv_slots);
@@ -1980,6 +2034,8 @@ int pii_engine_destroy(pii_engine* e) {
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
     for (auto& t : e->tev)
+        if (t) (void)hipEventDestroy(t);
+    for (auto& t : e->kev)
         if (t) (void)hipEventDestroy(t);
     if (e->stream && e->own_stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2063,6 +2119,11 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         tot += ms;
     }
     e->last_ms[5] = tot;
+    e->last_kms[0] = e->last_kms[1] = 0.f;
+    if (e->kev_valid) {
+        HIPCHK(hipEventElapsedTime(&e->last_kms[0], e->kev[0], e->kev[1]));
+        HIPCHK(hipEventElapsedTime(&e->last_kms[1], e->kev[2], e->kev[3]));
+    }
     if (totals) {
         totals[0] = e->h_totals[0];
         totals[1] = e->h_totals[1];
@@ -2080,6 +2141,23 @@ int pii_last_timings(pii_engine* e, float ms[6]) {
     if (!e || !ms) return PII_E_ARG;
     std::memcpy(ms, e->last_ms, sizeof(e->last_ms));
     return PII_OK;
+}
+
+int pii_last_queue_sizes(pii_engine* e, uint64_t* pairs, uint64_t* events) {
+    if (!e) return PII_E_ARG;
+    if (pairs) *pairs = e->h_totals[3];
+    if (events) *events = e->h_totals[4];
+    return PII_OK;
+}
+
+int pii_last_timings_ex(pii_engine* e, float* ms, uint32_t n) {
+    if (!e || (!ms && n)) return PII_E_ARG;
+    float all[8];
+    std::memcpy(all, e->last_ms, sizeof(e->last_ms));
+    all[6] = e->last_kms[0];
+    all[7] = e->last_kms[1];
+    for (uint32_t i = 0; i < n && i < 8; ++i) ms[i] = all[i];
+    return (int)std::min<uint32_t>(n, 8);
 }
 
 int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,

@@ -22,7 +22,8 @@ ERROR_NAMES = {PII_E_ARG: "PII_E_ARG", PII_E_RULES: "PII_E_RULES", PII_E_DEVICE:
                PII_E_CAPACITY: "PII_E_CAPACITY", PII_E_ORDER: "PII_E_ORDER", PII_E_NOMEM: "PII_E_NOMEM"}
 EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_type_name", "pii_context_group_type",
            "pii_last_error", "pii_scan_redact", "pii_scan_redact_device", "pii_sync", "pii_context_get",
-           "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings"]
+           "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
+           "pii_last_timings_ex", "pii_last_queue_sizes"]
 
 
 class PiiError(RuntimeError):
@@ -83,6 +84,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_histogram.argtypes = [P, U64, c.c_uint32]
     lib.pii_histogram_reset.argtypes = [P]
     lib.pii_last_timings.argtypes = [P, c.POINTER(c.c_float)]
+    lib.pii_last_timings_ex.argtypes = [P, c.POINTER(c.c_float), c.c_uint32]
+    lib.pii_last_queue_sizes.argtypes = [P, U64, U64]
     for name in EXPORTS:
         if name != "pii_last_error":
             getattr(lib, name).restype = c.c_int
@@ -209,6 +212,20 @@ class Engine:
         ms = (ctypes.c_float * 6)()
         self.lib.pii_last_timings(self.h, ms)
         return list(ms)
+
+    def kernel_timings(self) -> dict:
+        """Device time of the last call's roofline kernels alone (HIP events on the engine stream), ms."""
+        ms = (ctypes.c_float * 8)()
+        n = self.lib.pii_last_timings_ex(self.h, ms, 8)
+        if n < 0:
+            raise self._err(n, "pii_last_timings_ex")
+        return {"k_scan": float(ms[6]), "k_redact": float(ms[7])}
+
+    def queue_sizes(self) -> Tuple[int, int]:
+        """(candidate pairs, scan events) of the last call."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.pii_last_queue_sizes(self.h, ctypes.byref(a), ctypes.byref(b))
+        return int(a.value), int(b.value)
 
     # ------------------------------------------------------------------ context + histogram
     def context_get(self, slot: int) -> Tuple[int, int]:

@@ -123,6 +123,12 @@ int pii_histogram_reset(struct pii_engine* e);
 /* per-kernel device time of the last call, milliseconds (HIP events on the engine stream):
  * [0] scan [1] context [2] resolve [3] offsets [4] redact [5] total */
 int pii_last_timings(struct pii_engine* e, float ms[6]);
+/* the same six, then [6] the reverse DFA scan kernel (k_scan) and [7] the redaction kernel
+ * (k_redact) alone; fills min(n, 8) entries and returns that count */
+int pii_last_timings_ex(struct pii_engine* e, float* ms, uint32_t n);
+/* sizes of the last call's internal work queues: (start, pattern) candidate pairs and SCAN events
+ * (what the roofline accounting of k_scan counts as written) */
+int pii_last_queue_sizes(struct pii_engine* e, uint64_t* pairs, uint64_t* events);
 
 #ifdef __cplusplus
 }

@@ -2,7 +2,8 @@ import csv, json, sys
 tag = sys.argv[1]
 try:
     d = json.loads(open(f"gpurun_out/bench_{tag}.log").read().strip().splitlines()[-1])
-    print("value MB/s", d["value"], "ms/step", d["ms_per_step"], d["kernels_ms"], "roofline", d["roofline"]["achieved"], d["roofline"]["frac"])
+    print("value MB/s", d["value"], "ms/step", d["ms_per_step"], d.get("stages_ms"), d["kernels_ms"])
+    print("roofline", d["roofline"], "\nredact", d.get("roofline_redact"), "\ncpu", d.get("cpu_baseline"), "\nqueues", d.get("queues_per_step_per_gpu"))
 except Exception as e:
     print("no bench", e)
 try:
