@@ -1,0 +1,191 @@
+"""Host-side mirror of main_service (context-based-pii_amd/service.py): handler shapes, the
+reference's error strings, slot mapping, context TTL and realtime join/split.
+
+CPU tests drive PiiService with a test double of the engine whose results come from the oracle
+(test infrastructure only); the `gpu` tests drive it with the real HIP engine and compare the whole
+handler sequence with the oracle's replay of the reference handlers (main.py:344-466)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, pkg
+
+
+class OracleEngine:
+    """Engine test double: same Python surface as engine.Engine, results from oracle/pii_oracle.py."""
+
+    def __init__(self, cfg, n_slots=8, fail_code=None):
+        from oracle import pii_oracle as O
+        self.O, self.cfg = O, cfg
+        self.n_slots = n_slots
+        self.group_types = list(cfg.context_keywords.keys())
+        self.ctx = {}
+        self.fail_code = fail_code
+        self.calls = []
+
+    def context_get(self, slot):
+        return self.ctx.get(slot, (-1, 0))
+
+    def context_set(self, slot, g, ts):
+        self.ctx[slot] = (g, ts)
+
+    def scan_redact(self, texts, slots, roles, ts):
+        E = pkg("engine")
+        if self.fail_code is not None:
+            raise E.PiiError(self.fail_code, "injected")
+        self.calls.append(list(zip(slots, roles)))
+        outs, ctx_info = [], []
+        for t, s, r, now in zip(texts, slots, roles, ts):
+            et = None
+            if r == E.ROLE_CUSTOMER:
+                g, t0 = self.context_get(s)
+                if g >= 0 and now - t0 < 90_000_000:
+                    et = self.group_types[g]
+            red, _ = self.O.redact(t, self.cfg, et)
+            info = -1
+            if r == E.ROLE_AGENT:
+                hit = self.O.extract_expected_pii(t, self.cfg)
+                if hit:
+                    info = self.group_types.index(hit)
+                    self.context_set(s, info, now)
+            elif et is not None:
+                info = self.group_types.index(et)
+            outs.append(red)
+            ctx_info.append(info)
+        data, offs = E.pack(outs)
+        return E.BatchResult(data, offs, np.zeros(0, E.SPAN_DTYPE), np.array(ctx_info, np.int16))
+
+
+class Clock:
+    def __init__(self, t=1_760_000_000.0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+@pytest.fixture
+def svc(oracle_cfg):
+    S = pkg("service")
+    clock = Clock()
+    s = S.PiiService(engine=OracleEngine(oracle_cfg), clock=clock)
+    s._clock = clock
+    return s
+
+
+def test_handler_shapes_and_400s(svc):
+    assert svc.handle_agent_utterance(None)[1] == 400
+    assert svc.handle_agent_utterance({"transcript": "x"}) == ({"error": "Missing conversation_id or transcript"}, 400)
+    assert svc.handle_customer_utterance({"conversation_id": "c"})[1] == 400
+    assert svc.redact_utterance_realtime({"conversation_id": "c"}) == ({"error": "Missing conversation_id or utterance"}, 400)
+    body, code = svc.handle_agent_utterance({"conversation_id": "c1", "transcript": "Could I get your email address?"})
+    assert code == 200 and set(body) == {"redacted_transcript", "context_stored"} and body["context_stored"] is True
+    body, code = svc.handle_customer_utterance({"conversation_id": "c1", "transcript": "it is jane.doe@example.com"})
+    assert body == {"redacted_transcript": "it is [EMAIL_ADDRESS]", "context_used": True}
+    body, _ = svc.handle_customer_utterance({"conversation_id": "c2", "transcript": "hi"})
+    assert body == {"redacted_transcript": "hi", "context_used": False}
+
+
+def test_context_ttl_and_persistence(svc):
+    svc.handle_agent_utterance({"conversation_id": "c", "transcript": "What is your card number?"})
+    svc._clock.t += 89.0
+    assert svc.handle_customer_utterance({"conversation_id": "c", "transcript": "ok"})[0]["context_used"]
+    svc.handle_agent_utterance({"conversation_id": "c", "transcript": "Thanks."})      # a miss keeps the record
+    assert svc.handle_customer_utterance({"conversation_id": "c", "transcript": "ok"})[0]["context_used"]
+    svc._clock.t += 2.0                                                                  # 91 s after the hit
+    assert not svc.handle_customer_utterance({"conversation_id": "c", "transcript": "ok"})[0]["context_used"]
+
+
+def test_error_strings_follow_the_reference(oracle_cfg):
+    S, E = pkg("service"), pkg("engine")
+    for code, prefix in [(E.PII_E_DEVICE, "[DLP_API_CALL_ERROR]"), (E.PII_E_RULES, "[DLP_TEMPLATE_NOT_FOUND_ERROR]"),
+                         (E.PII_E_NOMEM, "[DLP_PROCESSING_ERROR]"), (E.PII_E_ARG, "[DLP_PROCESSING_ERROR]")]:
+        s = S.PiiService(engine=OracleEngine(oracle_cfg, fail_code=code))
+        assert s.call_dlp_for_redaction("my ssn", None) == f"{prefix} my ssn"
+        body, code200 = s.handle_customer_utterance({"conversation_id": "c", "transcript": "t"})
+        assert code200 == 200 and body["redacted_transcript"] == f"{prefix} t"
+
+
+def test_stateless_seam_and_extract(svc, oracle_cfg):
+    from oracle import pii_oracle as O
+    t = "card 4141-1212-2323-5009 and code 123"
+    for ctx in (None, {"expected_pii_type": "CVV_NUMBER"}, {"expected_pii_type": "CREDIT_CARD_NUMBER"}):
+        red, _ = O.redact(t.encode(), oracle_cfg, ctx and ctx["expected_pii_type"])
+        assert svc.call_dlp_for_redaction(t, ctx) == red.decode()
+    assert svc.extract_expected_pii("What's the CVV on the back?") == O.extract_expected_pii(
+        b"What's the CVV on the back?", oracle_cfg)
+    assert svc.extract_expected_pii("Thanks") is None
+
+
+def test_slot_map_lru_evicts_and_clears():
+    S = pkg("service")
+    evicted = []
+    m = S.SlotMap(4, on_evict=evicted.append)
+    a, b, c = m.get("a"), m.get("b"), m.get("c")
+    assert sorted((a, b, c)) == [1, 2, 3]                 # slot 0 reserved
+    m.get("a")                                            # a becomes most recent
+    d = m.get("d")
+    assert d == b and evicted == [b] and m.peek("b") is None and m.get("a") == a
+
+
+def test_realtime_join_split(svc, oracle_cfg):
+    from oracle import pii_oracle as O
+    agent = "Please confirm your phone number."
+    svc.handle_agent_utterance({"conversation_id": "r", "transcript": agent})
+    body, _ = svc.redact_utterance_realtime({"conversation_id": "r", "utterance": "it's 555-867-5309"})
+    exp = O.realtime_redact(agent.encode(), b"it's 555-867-5309", oracle_cfg, "PHONE_NUMBER")
+    assert body == {"redacted_utterance": exp.decode()}
+    body, _ = svc.redact_utterance_realtime({"conversation_id": "none", "utterance": "hi 555-867-5309"})
+    assert body["redacted_utterance"] == O.redact(b"hi 555-867-5309", oracle_cfg, None)[0].decode()
+
+
+def _replay_handlers(svc, entries, cid):
+    out = []
+    for e in entries:
+        d = {"conversation_id": cid, "transcript": e["text"]}
+        body, _ = (svc.handle_agent_utterance(d) if e["role"] == "AGENT" else svc.handle_customer_utterance(d))
+        out.append(body["redacted_transcript"])
+    return out
+
+
+def _oracle_replay(oracle_cfg, entries, cid):
+    from oracle import pii_oracle as O
+    rows = [(cid, O.ROLE_AGENT if e["role"] == "AGENT" else O.ROLE_CUSTOMER, e["text"].encode(), e["ts"])
+            for e in entries]
+    return [r[0].decode() for r in O.process_rows(rows, oracle_cfg)]
+
+
+def test_handler_replay_double(svc, oracle_cfg):
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    for name, t in tr.items():
+        assert _replay_handlers(svc, t["entries"], t["conversation_id"]) == _oracle_replay(
+            oracle_cfg, t["entries"], t["conversation_id"])
+
+
+@pytest.mark.gpu
+def test_service_on_gpu_matches_oracle(oracle_cfg):
+    """The real engine behind the reference's handler sequence, the stateless seam, the realtime
+    handler and the batched ingest path -- all vs the oracle replay of main.py:344-466."""
+    from oracle import pii_oracle as O
+    S = pkg("service")
+    clock = Clock()
+    svc = S.PiiService(n_slots=64, clock=clock)
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    for name, t in tr.items():
+        assert _replay_handlers(svc, t["entries"], t["conversation_id"]) == _oracle_replay(
+            oracle_cfg, t["entries"], t["conversation_id"]), name
+    for name, t in tr.items():
+        rows = [{"conversation_id": "b" + t["conversation_id"], "participant_role": e["role"], "text": e["text"],
+                 "start_timestamp_usec": e["ts"]} for e in t["entries"]]
+        assert svc.process_batch(rows) == _oracle_replay(oracle_cfg, t["entries"], "b" + t["conversation_id"])
+    t = "card 4141-1212-2323-5009, cvv 123, ssn 123-45-6789"
+    for g in [None] + list(oracle_cfg.context_keywords.keys()):
+        ctx = {"expected_pii_type": g} if g else None
+        assert svc.call_dlp_for_redaction(t, ctx) == O.redact(t.encode(), oracle_cfg, g)[0].decode(), g
+    agent = "Could you read me the IMEI of the device?"
+    svc.handle_agent_utterance({"conversation_id": "rt", "transcript": agent})
+    body, _ = svc.redact_utterance_realtime({"conversation_id": "rt", "utterance": "sure 490154203237518"})
+    assert body["redacted_utterance"] == O.realtime_redact(agent.encode(), b"sure 490154203237518", oracle_cfg,
+                                                           O.extract_expected_pii(agent.encode(), oracle_cfg)).decode()
