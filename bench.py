@@ -52,27 +52,29 @@ def _cpu_work(rng):
 
 
 def cpu_baseline(bank, seconds: float = 15.0):
-    """The oracle (Python re + validators), multi-process over whole conversations on the host."""
+    """The oracle (Python re + validators), multi-process over whole conversations on the host.
+    Calibrated on one 10-conversation block, then sized to about `seconds` of wall time."""
     cores = min(16, os.cpu_count() or 1)
-    meta = synth.corpus_meta(4000, 100, bank, seed=synth.SEED + 7)
+    probe = synth.corpus_meta(10, 100, bank, seed=synth.SEED + 7)
+    pdata = synth.gather_bytes(probe, bank)
+    _cpu_init(pdata, probe.offsets.astype(np.int64), probe.role, probe.conv_slot, probe.ts_us)
+    dt, nb = _cpu_work((0, probe.n))
+    conv_rate = 10 / max(dt, 1e-6)                       # conversations / s / core
+    n_conv = int(min(30000, max(cores * 4, conv_rate * cores * seconds * 0.5)))   # probe is optimistic ~2x
+    meta = synth.corpus_meta(n_conv, 100, bank, seed=synth.SEED + 7)
     data = synth.gather_bytes(meta, bank)
     offs = meta.offsets.astype(np.int64)
-    # calibrate on one conversation block, then size the sample to ~`seconds` of wall time
-    _cpu_init(data, offs, meta.role, meta.conv_slot, meta.ts_us)
-    dt, nb = _cpu_work((0, 1000))
-    rate1 = nb / max(dt, 1e-6)
-    target_bytes = rate1 * cores * seconds
-    n_conv = int(min(4000, max(cores, target_bytes / (nb / 10))))
     chunks = [(i * 100, (i + 1) * 100) for i in range(n_conv)]
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(cores, initializer=_cpu_init, initargs=(data, offs, meta.role, meta.conv_slot, meta.ts_us)) as pool:
-        res = pool.map(_cpu_work, chunks, chunksize=max(1, len(chunks) // (cores * 4)))
+        res = pool.map(_cpu_work, chunks, chunksize=max(1, len(chunks) // (cores * 8)))
     wall = time.perf_counter() - t0
     nbytes = sum(b for _, b in res)
     return {"value": round(nbytes / wall / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
             "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e6:.1f} MB) of the same synthetic "
-                      f"distribution, oracle/pii_oracle.py process_rows, multiprocessing fork pool, wall {wall:.1f}s"}
+                      f"distribution, oracle/pii_oracle.py process_rows, multiprocessing fork pool of {cores}, "
+                      f"wall {wall:.1f}s"}
 
 
 def source_digest() -> str:
