@@ -861,11 +861,18 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     # ---- FIRST: one anchored leftmost-first DFA per detector pattern ----
     first = []
     min_len = 1 << 30
+    # window_ok: no detector can consume '\n' or test a text edge (\A, \Z).  Then no match crosses
+    # the "\n" that joins a re-scan window, and a match inside one utterance is the same
+    # match inside the window, which is what lets the engine re-scan windows incrementally.
+    window_ok = 1
     for p in rules.patterns:
         n2 = NFA()
         st = add_pattern(n2, p.pattern, p.pid, reverse=False)
         first.append(build_first_dfa(n2, st))
         min_len = min(min_len, _min_len(parse(p.pattern)))
+        for k, b, cs in zip(n2.kind, n2.b, n2.cs):
+            if (k == CHAR and cs & NEWLINE) or (k == ASSERT and b in (A_BEGIN, A_END)):
+                window_ok = 0
 
     # ---- variants (context merge, main.py:609-686) + HOT rule DFAs ----
     T = len(rules.type_names)
@@ -972,7 +979,7 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     meta = np.array([P, G, T, V,
                      scan_d.n_states, scan_d.n_classes + 1, scan_d.start,
                      scan_k.n_states, scan_k.n_classes + 1, scan_k.start,
-                     len(hot_rules), min_len, scan_budget, 0, 0, 0], dtype=np.int64)
+                     len(hot_rules), min_len, scan_budget, window_ok, 0, 0], dtype=np.int64)
     S = OrderedDict()
     S["meta"] = meta
     S["scan.cmap2"] = cmap2

@@ -45,7 +45,7 @@ constexpr uint32_t BYTES_PER_LANE = 1024;
 constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
-enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8 };
+enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16 };
 
 struct Event {
     uint32_t pos;   // candidate start, relative to the batch base
@@ -80,6 +80,7 @@ struct RulesDev {
     const uint16_t* excl_ids;
     const uint32_t* tok_off;     // [T+1] into tok_bytes: "[NAME]"
     const uint8_t* tok_bytes;
+    uint32_t nl_off;             // tok_bytes[nl_off] = '\n' (the re-scan window separator)
 };
 
 // ------------------------------------------------------------------------------- k_chunk_index
@@ -89,7 +90,7 @@ struct RulesDev {
 __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role, uint32_t n_utt,
                               uint32_t n_chunks, int kw_always, uint32_t* __restrict__ first_utt,
                               uint32_t* __restrict__ out_len, uint32_t* __restrict__ n_find,
-                              int16_t* __restrict__ kw) {
+                              int16_t* __restrict__ kw, uint32_t* __restrict__ wc_n) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u > n_utt) return;
     const uint64_t base = offs[0];
@@ -103,6 +104,7 @@ __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* 
         out_len[u] = (uint32_t)(offs[u + 1] - offs[u]);
         n_find[u] = 0;
         kw[u] = (int16_t)((role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1);
+        if (wc_n) wc_n[u] = 0;
     }
 }
 
@@ -424,7 +426,8 @@ __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __
                             uint32_t n_slots, int64_t ttl_us, const uint32_t* __restrict__ incl,
                             const int32_t* __restrict__ agg_v, const uint32_t* __restrict__ agg_f,
                             const int32_t* __restrict__ st_group, const int64_t* __restrict__ st_ts,
-                            int16_t* __restrict__ ctx, int32_t* __restrict__ commit) {
+                            int16_t* __restrict__ ctx, int32_t* __restrict__ commit,
+                            int16_t* __restrict__ win_ctx) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= n_utt) return;
     const uint32_t sl = slot[u];
@@ -440,8 +443,8 @@ __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __
         if (prev < 0 && !run_started_in_blk) prev = ctx_carry(agg_v, agg_f, blk);
     }
     const uint8_t r = role[u];
-    int16_t used = -1;
-    if (r == PII_ROLE_CUSTOMER && sl < n_slots) {
+    int16_t used = -1, live = -1;
+    if ((r == PII_ROLE_CUSTOMER || win_ctx) && sl < n_slots) {
         int32_t g;
         int64_t t;
         if (prev >= 0) {
@@ -452,8 +455,12 @@ __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __
             t = st_ts[sl];
         }
         const int64_t now = ts ? ts[u] : 0;
-        if (g >= 0 && (ts == nullptr || now - t < ttl_us)) used = (int16_t)g;
+        if (g >= 0 && (ts == nullptr || now - t < ttl_us)) live = (int16_t)g;
+        if (r == PII_ROLE_CUSTOMER) used = live;
     }
+    // the re-scan window of row u uses the context a request right after u would GET (main.py:403):
+    // an AGENT row's own hit, else the live record
+    if (win_ctx) win_ctx[u] = (r == PII_ROLE_AGENT && kw[u] >= 0) ? kw[u] : live;
     ctx[u] = (r == PII_ROLE_AGENT) ? kw[u] : used;
     // last row of the run: the latest hit of the whole run (to be committed)
     const bool last = (u == n_utt - 1) || slot[u + 1] != sl;
@@ -507,13 +514,16 @@ struct PairRes {       // one (start, pattern) candidate (8 B); its FIRST end li
 
 // LDS images of rule tables, one per kernel (only what that kernel reads, so the pair kernels keep
 // two 1024-thread workgroups per CU).  Sections are 16-byte aligned; off[] are byte offsets.
-constexpr int IMG_MAX = 12;
+constexpr int IMG_MAX = 16;
 struct LdsImage {
     uint32_t off[IMG_MAX];
     uint32_t total;    // bytes, multiple of 16
 };
 enum { FI_TRANS, FI_CMAP, FI_DESC, FI_N };
-enum { EV_TRANS, EV_CMAP, EV_HDESC, EV_HRULE, EV_DTYPE, EV_DVAL, EV_DLIK, EV_ROFF, EV_RIDS, EV_N };
+enum { EV_TRANS, EV_CMAP, EV_HDESC, EV_HRULE, EV_DTYPE, EV_DVAL, EV_DLIK, EV_ROFF, EV_RIDS, EV_THOT, EV_N };
+// k_win_select: everything k_select reads + the HOT automata and the variants' hotword rule lists
+enum { WS_TRANS, WS_CMAP, WS_HDESC, WS_HRULE, WS_DTYPE, WS_DLIK, WS_VEN, WS_VMIN, WS_DEX, WS_XOFF, WS_XIDS,
+       WS_TOKOFF, WS_ROFF, WS_RIDS, WS_N };
 enum { SE_DTYPE, SE_VEN, SE_VMIN, SE_DEX, SE_XOFF, SE_XIDS, SE_TOKOFF, SE_N };
 
 constexpr int PAIR_BLOCK = 1024;
@@ -1140,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t* __restrict__ span_offs,
                            uint32_t n_utt, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
                            uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count,
-                           const uint64_t* __restrict__ ev_count) {
+                           const uint64_t* __restrict__ ev_count, const uint64_t* __restrict__ wf_count) {
     const uint64_t ob = out_offs[n_utt], ns = span_offs[n_utt];
     if (ob > out_cap || ns > span_cap) atomicOr(err, (uint32_t)ERR_CAPACITY);
     totals[0] = ob;
@@ -1148,6 +1158,7 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
     totals[2] = *err;
     totals[3] = *pair_count;
     totals[4] = ev_count ? *ev_count : 0;
+    totals[5] = wf_count ? *wf_count : 0;
 }
 
 // ---------------------------------------------------------------------------------- k_redact
@@ -1183,6 +1194,108 @@ __device__ uint32_t redact_byte_slow(const RulesDev& R, const uint8_t* src, cons
     return src[pin + (rel - pout)];
 }
 
+// Output assembly shared by k_redact and k_win_redact.  The piece table (s_pout = tile-relative
+// output offset of each piece, s_psrc = ABSOLUTE device address of its first byte; a sentinel
+// s_pout[total_p] = tile output length) is in LDS; a block -> piece table is built, then lane i
+// assembles aligned 16-byte output blocks i, i+blockDim, ...  Returns false (nothing written) when
+// the piece table did not fit (the caller's slow path runs instead).
+__device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint64_t* s_psrc, uint32_t total_p,
+                                              uint16_t* s_bp, uint32_t* s_wsum, uint8_t* __restrict__ out,
+                                              int64_t out_lo, int64_t out_hi) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t omis = (int64_t)((uintptr_t)out & 15);
+    const int64_t q_lo = (out_lo + omis) >> 4;
+    const int64_t q_hi = out_hi > out_lo ? (out_hi - 1 + omis) >> 4 : q_lo - 1;
+    const int64_t nblk = q_hi - q_lo + 1;
+    const bool table = nblk > 0 && nblk <= BLK_MAX;
+    if (table) {
+        // block b's first valid byte is rf(b) = max(0, 16b - e0); piece(b) = max{p : pout[p] <= rf(b)}
+        const uint32_t e0 = (uint32_t)((out_lo + omis) - 16 * q_lo);
+        constexpr int PER = BLK_MAX / REDACT_BLOCK;
+        for (int i = tid; i < BLK_MAX; i += REDACT_BLOCK) s_bp[i] = 0;
+        __syncthreads();
+        for (uint32_t p = tid; p < total_p; p += REDACT_BLOCK) {
+            const uint32_t k = s_pout[p] == 0 ? 0u : (s_pout[p] + e0 + 15) >> 4;
+            const uint32_t kn = p + 1 == total_p ? 0xffffffffu : (s_pout[p + 1] == 0 ? 0u : (s_pout[p + 1] + e0 + 15) >> 4);
+            if (kn != k && k < (uint32_t)nblk) s_bp[k] = (uint16_t)p;      // last piece with this key
+        }
+        __syncthreads();
+        // prefix max over the block table: PER entries per lane, then across lanes
+        uint32_t m = 0;
+        for (int j = 0; j < PER; ++j) m = max(m, (uint32_t)s_bp[tid * PER + j]);
+        uint32_t incl_m = m;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl_m, d);
+            if (lane >= d) incl_m = max(incl_m, o);
+        }
+        if (lane == 63) s_wsum[wid] = incl_m;
+        __syncthreads();
+        uint32_t run = 0;
+        for (int w = 0; w < wid; ++w) run = max(run, s_wsum[w]);
+        const uint32_t excl_m = __shfl_up(incl_m, 1);
+        run = max(run, lane ? excl_m : 0u);
+        for (int j = 0; j < PER; ++j) {
+            run = max(run, (uint32_t)s_bp[tid * PER + j]);
+            s_bp[tid * PER + j] = (uint16_t)run;
+        }
+        __syncthreads();
+    }
+    if (total_p == 0) return;
+    uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
+    const int64_t span = out_hi - out_lo;
+    for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
+        const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
+        const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
+        const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
+        uint32_t pi;
+        if (table) {
+            pi = s_bp[q - q_lo];
+        } else {
+            const uint32_t rs = (uint32_t)(r0 + b_lo);
+            uint32_t lo_i = 0, hi_i = total_p - 1;       // last piece with s_pout <= rs
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                if (s_pout[mid] <= rs) lo_i = mid;
+                else hi_i = mid - 1;
+            }
+            pi = lo_i;
+        }
+        uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
+        uint64_t qsrc = s_psrc[pi];
+        uint4 v = make_uint4(0, 0, 0, 0);
+        for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
+            const int lo = max(b_lo, (int)((int64_t)qs - r0));
+            const int hi = min(b_hi, (int)((int64_t)qe - r0));
+            if (hi > lo) {
+                const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
+                const uint4 w = load16(reinterpret_cast<const uint8_t*>(qsrc) + delta, lo, hi);
+                if (lo == 0 && hi == 16) {
+                    v = w;
+                } else {
+                    v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
+                    v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
+                    v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
+                    v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
+                }
+            }
+            if ((int64_t)qe >= r0 + b_hi) break;
+            ++pi;
+            qs = qe;
+            qe = s_pout[pi + 1];
+            qsrc = s_psrc[pi];
+        }
+        if (b_lo == 0 && b_hi == 16) {
+            op[q] = v;
+        } else {
+            uint8_t* ob = out - omis + q * 16;
+            const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
+        }
+    }
+}
+
 __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ offs, uint32_t n_utt,
                                                          const pii_span* __restrict__ fd,
@@ -1193,7 +1306,7 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
                                                          pii_span* __restrict__ spans,
                                                          uint32_t* __restrict__ hist_part) {
     __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (tile relative)
-    __shared__ uint64_t s_psrc[PIECE_MAX + 1];     // piece source: text position, or bit 63 | token offset
+    __shared__ uint64_t s_psrc[PIECE_MAX + 1];     // piece source address (text or token table)
     __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
     __shared__ uint16_t s_bp[BLK_MAX];             // output block -> piece holding its first byte
     __shared__ uint32_t sh_hist[256];
@@ -1234,11 +1347,11 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
     if (mine) {
         uint32_t pb = wpre + incl - cnt;
         uint32_t po = (uint32_t)((int64_t)o_abs - out_lo);
-        const uint64_t so = s_abs;
+        const uint64_t src0 = (uint64_t)(uintptr_t)(text + s_abs);
         if (nf == 0) {
             if (staged) {
                 s_pout[pb] = po;
-                s_psrc[pb] = so;
+                s_psrc[pb] = src0;
             }
         } else {
             const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
@@ -1251,11 +1364,11 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
                 const uint32_t t0 = R.tok_off[F.info_type];
                 if (staged) {
                     s_pout[pb] = po;
-                    s_psrc[pb] = so + pin;
+                    s_psrc[pb] = src0 + pin;
                     po += F.start - pin;
                     ++pb;
                     s_pout[pb] = po;
-                    s_psrc[pb] = (1ull << 63) | t0;
+                    s_psrc[pb] = (uint64_t)(uintptr_t)(R.tok_bytes + t0);
                     po += R.tok_off[F.info_type + 1] - t0;
                     ++pb;
                 }
@@ -1263,106 +1376,15 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
             }
             if (staged) {
                 s_pout[pb] = po;
-                s_psrc[pb] = so + pin;
+                s_psrc[pb] = src0 + pin;
             }
         }
     }
     if (tid == 0 && staged) s_pout[total_p] = (uint32_t)(out_hi - out_lo);   // sentinel
     __syncthreads();
-    const int64_t omis = (int64_t)((uintptr_t)out & 15);
-    const int64_t q_lo = (out_lo + omis) >> 4;
-    const int64_t q_hi = out_hi > out_lo ? (out_hi - 1 + omis) >> 4 : q_lo - 1;
-    const int64_t nblk = q_hi - q_lo + 1;
-    const bool table = staged && nblk > 0 && nblk <= BLK_MAX;
-    if (table) {
-        // block b's first valid byte is rf(b) = max(0, 16b - e0); piece(b) = max{p : pout[p] <= rf(b)}
-        const uint32_t e0 = (uint32_t)((out_lo + omis) - 16 * q_lo);
-        constexpr int PER = BLK_MAX / REDACT_BLOCK;
-        for (int i = tid; i < BLK_MAX; i += REDACT_BLOCK) s_bp[i] = 0;
-        __syncthreads();
-        for (uint32_t p = tid; p < total_p; p += REDACT_BLOCK) {
-            const uint32_t k = s_pout[p] == 0 ? 0u : (s_pout[p] + e0 + 15) >> 4;
-            const uint32_t kn = p + 1 == total_p ? 0xffffffffu : (s_pout[p + 1] == 0 ? 0u : (s_pout[p + 1] + e0 + 15) >> 4);
-            if (kn != k && k < (uint32_t)nblk) s_bp[k] = (uint16_t)p;      // last piece with this key
-        }
-        __syncthreads();
-        // prefix max over the block table: PER entries per lane, then across lanes
-        uint32_t m = 0;
-        for (int j = 0; j < PER; ++j) m = max(m, (uint32_t)s_bp[tid * PER + j]);
-        uint32_t incl_m = m;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(incl_m, d);
-            if (lane >= d) incl_m = max(incl_m, o);
-        }
-        if (lane == 63) s_wsum[wid] = incl_m;
-        __syncthreads();
-        uint32_t run = 0;
-        for (int w = 0; w < wid; ++w) run = max(run, s_wsum[w]);
-        const uint32_t excl_m = __shfl_up(incl_m, 1);
-        run = max(run, lane ? excl_m : 0u);
-        for (int j = 0; j < PER; ++j) {
-            run = max(run, (uint32_t)s_bp[tid * PER + j]);
-            s_bp[tid * PER + j] = (uint16_t)run;
-        }
-        __syncthreads();
-    }
-    if (staged && total_p > 0) {
-        uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
-        const int64_t span = out_hi - out_lo;
-        for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
-            const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
-            const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
-            const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
-            uint32_t pi;
-            if (table) {
-                pi = s_bp[q - q_lo];
-            } else {
-                const uint32_t rs = (uint32_t)(r0 + b_lo);
-                uint32_t lo_i = 0, hi_i = total_p - 1;       // last piece with s_pout <= rs
-                while (lo_i < hi_i) {
-                    const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                    if (s_pout[mid] <= rs) lo_i = mid;
-                    else hi_i = mid - 1;
-                }
-                pi = lo_i;
-            }
-            uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
-            uint64_t qsrc = s_psrc[pi];
-            uint4 v = make_uint4(0, 0, 0, 0);
-            for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
-                const int lo = max(b_lo, (int)((int64_t)qs - r0));
-                const int hi = min(b_hi, (int)((int64_t)qe - r0));
-                if (hi > lo) {
-                    const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
-                    const uint8_t* src = (qsrc >> 63) ? R.tok_bytes + (uint32_t)qsrc + delta
-                                                      : text + (qsrc + delta);
-                    const uint4 w = load16(src, lo, hi);
-                    if (lo == 0 && hi == 16) {
-                        v = w;
-                    } else {
-                        v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
-                        v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
-                        v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
-                        v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
-                    }
-                }
-                if ((int64_t)qe >= r0 + b_hi) break;
-                ++pi;
-                qs = qe;
-                qe = s_pout[pi + 1];
-                qsrc = s_psrc[pi];
-            }
-            if (b_lo == 0 && b_hi == 16) {
-                op[q] = v;
-            } else {
-                uint8_t* ob = out - omis + q * 16;
-                const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
-            }
-        }
-    } else if (!staged) {
+    if (staged) {
+        tile_assemble(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
+    } else {
         // too many pieces: one wavefront per utterance, byte-granular
         for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
             const uint32_t uu = u0 + i;
@@ -1396,6 +1418,681 @@ __global__ __launch_bounds__(256) void k_hist_reduce(const uint32_t* __restrict_
     if (threadIdx.x == 0) {
         const unsigned long long tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
         if (tot) atomicAdd(&hist[t], tot);
+    }
+}
+
+// ============================================================================ window re-scan (a12)
+// README.md:131-134 / SURVEY A.9: after each utterance the aggregator re-redacts "\n".join(last N
+// utterances) with the conversation's current expected_pii_type.  Incremental form used here:
+// when no detector can consume '\n' or test a text edge (compiler `window_ok`), a match inside the
+// window lies inside one utterance and equals that utterance's own match, so each utterance is
+// scanned ONCE (its new bytes), and its finditer-resolved, validator-passing candidates are kept
+// resident in HBM with a bit per hotword rule for the proximity windows clipped to the utterance.
+// A window then only (1) re-evaluates hotword windows that reach across a "\n" into a neighbour
+// utterance (the halo), (2) applies the window's context variant (likelihoods, min likelihood,
+// exclusion, overlap) and (3) writes the redacted window.  Candidates of different utterances never
+// overlap, so exclusion and overlap resolution stay per utterance.
+constexpr int WN_MAX = 8;          // largest window (utterances)
+constexpr int WIN_TILE = 64;       // windows per k_win_redact workgroup
+
+struct WCand {          // one resident candidate (16 B)
+    uint32_t s, e;      // match [s, e), relative to its utterance
+    uint16_t p;         // detector pattern
+    uint16_t pad;
+    uint32_t hot;       // bit h: hotword rule h hits inside the utterance (windows clipped to it)
+};
+struct WDesc {          // one resident utterance of a conversation's history ring (16 B)
+    uint32_t off;       // arena offset (16-aligned): nc WCands, then the text bytes
+    uint32_t len;
+    uint32_t nc;
+    uint32_t pad;
+};
+struct WNew {           // commit plan of a batch row that enters its conversation's ring
+    uint32_t off;       // arena offset, ~0 = the row does not enter the ring
+    uint32_t ri;        // descriptor index
+    uint32_t cnt;       // (last row of a run) live entries after the commit
+    uint32_t head;      // (last row of a run) next descriptor index after the commit
+};
+struct WinRing {        // per-conversation history in HBM (replaces the aggregator's Redis list)
+    WDesc* desc;        // [slots * N]
+    uint32_t* cnt;      // [slots] live entries (<= N)
+    uint32_t* head;     // [slots] next descriptor index (newest = head - 1 mod N)
+    uint8_t* arena;     // [slots * slot_bytes]
+    uint32_t N, slot_bytes, n_slots, pad;
+};
+struct WinBatch {       // this call's rows and their freshly built candidate lists
+    const uint8_t* text;
+    const uint64_t* offs;
+    const uint32_t* slot;
+    const WCand* wc;
+    const uint32_t* wc_first;
+    const uint32_t* wc_n;
+    uint32_t n_utt;
+};
+struct WEntry {
+    const uint8_t* t;
+    const WCand* c;
+    uint32_t len, nc;
+};
+
+// The window of row u, oldest first: the newest ring entries of u's conversation, then u's
+// same-conversation predecessors in the batch, then u.  Returns the entry count (>= 1).
+__device__ __forceinline__ int win_entries(const WinRing& W, const WinBatch& B, uint32_t u, WEntry* E) {
+    const uint32_t sl = B.slot[u];
+    uint32_t m = 0;
+    while (m + 1 < W.N && u >= m + 1 && B.slot[u - m - 1] == sl) ++m;
+    uint32_t r = 0;
+    if (m + 1 < W.N && sl < W.n_slots) r = min(W.N - 1 - m, W.cnt[sl]);
+    int nw = 0;
+    if (r) {
+        const uint32_t head = W.head[sl];
+        const uint8_t* ar = W.arena + (size_t)sl * W.slot_bytes;
+        for (uint32_t i = 0; i < r; ++i) {
+            const WDesc D = W.desc[(size_t)sl * W.N + (head + W.N - r + i) % W.N];
+            E[nw].t = ar + D.off + 16u * D.nc;
+            E[nw].c = reinterpret_cast<const WCand*>(ar + D.off);
+            E[nw].len = D.len;
+            E[nw].nc = D.nc;
+            ++nw;
+        }
+    }
+    for (uint32_t i = 0; i <= m; ++i) {
+        const uint32_t v = u - m + i;
+        const uint64_t a = B.offs[v];
+        E[nw].t = B.text + a;
+        E[nw].nc = B.wc_n[v];
+        E[nw].c = B.wc + (E[nw].nc ? B.wc_first[v] : 0u);
+        E[nw].len = (uint32_t)(B.offs[v + 1] - a);
+        ++nw;
+    }
+    return nw;
+}
+
+// Unanchored HOT DFA over window positions [lo, hi) (entry j starts at window offset O[j]; entries
+// are joined by '\n'), window edges as text edges: the proximity test of a candidate whose window
+// reaches into a neighbour utterance.
+__device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WEntry* E, const uint32_t* O, int nw,
+                            uint32_t lo, uint32_t hi) {
+    const uint16_t* tr = pool.trans + d[0];
+    const uint8_t* cm = pool.cmap + d[2];
+    const uint32_t nc = (uint32_t)d[3];
+    uint32_t st = (uint32_t)d[4];
+    for (int j = 0; j < nw; ++j) {
+        const uint32_t sl = O[j], sh = O[j] + E[j].len;
+        if (sh < lo) continue;
+        if (sl >= hi) break;
+        const int a = (int)(max(lo, sl) - sl), b = (int)(min(hi, sh) - sl);
+        const uint8_t* t = E[j].t;
+        PII_FOR_BYTES(t, a, b, {
+            const uint32_t x = tr[st * nc + cm[c]];
+            if (x & 0x4000u) return true;
+            st = x & DFA_STATE_MASK;
+        })
+        if (j + 1 < nw && sh >= lo && sh < hi) {
+            const uint32_t x = tr[st * nc + cm['\n']];
+            if (x & 0x4000u) return true;
+            st = x & DFA_STATE_MASK;
+        }
+    }
+    return (tr[st * nc + nc - 1] & 0x4000u) != 0;
+}
+
+// per matched pair: validator + every hotword rule the pattern's type has in ANY context variant,
+// proximity windows clipped to the utterance -> PairRes.lik = 0 valid / -1 invalid, phot = rule bits
+__global__ __launch_bounds__(PAIR_BLOCK) void k_win_eval(const uint4* __restrict__ img, const LdsImage li,
+                                                         const uint8_t* __restrict__ text0,
+                                                         const uint64_t* __restrict__ offs,
+                                                         const unsigned long long* __restrict__ pair_count,
+                                                         uint64_t pair_cap, const uint32_t* __restrict__ matched,
+                                                         const uint32_t* __restrict__ mcount, uint32_t nseg,
+                                                         const EvLoc* __restrict__ evloc,
+                                                         const int32_t* __restrict__ pend,
+                                                         PairRes* __restrict__ pres, uint32_t* __restrict__ phot) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
+    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
+    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[EV_DTYPE]);
+    const uint8_t* dval = lb + li.off[EV_DVAL];
+    const uint32_t* thot = reinterpret_cast<const uint32_t*>(lb + li.off[EV_THOT]);
+    const uint8_t* text = text0 + offs[0];
+    __shared__ uint32_t s_mp[PAIR_WAVES + 1];
+    const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg * PAIR_WAVES);
+    for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int w = 0; w < PAIR_WAVES; ++w) {
+                s_mp[w] = run;
+                run += mcount[g * PAIR_WAVES + w];
+            }
+            s_mp[PAIR_WAVES] = run;
+        }
+        __syncthreads();
+        const uint32_t m = s_mp[PAIR_WAVES];
+        for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) {
+            int w = 0;
+            while (w + 1 < PAIR_WAVES && s_mp[w + 1] <= k) ++w;
+            const uint32_t i = matched[(uint64_t)(g * PAIR_WAVES + w) * seg + (k - s_mp[w])];
+            const PairRes P = pres[i];
+            const EvLoc Lc = evloc[P.ev];
+            const uint8_t* t0 = text + Lc.ustart;
+            const int L = (int)(Lc.uend - Lc.ustart);
+            const int s = (int)(Lc.s - Lc.ustart), e = pend[i];
+            int lik = -1;
+            uint32_t hot = 0;
+            if (validate(dval[P.p], t0 + s, e - s)) {
+                lik = 0;
+                uint32_t mask = thot[dtype[P.p]];
+                while (mask) {
+                    const int h = __builtin_ctz(mask);
+                    mask &= mask - 1;
+                    const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
+                    bool hit = false;
+                    if (wb > 0) hit = hot_run(pool, hdesc + 8 * h, t0, s - wb > 0 ? s - wb : 0, s);
+                    if (!hit && wa > 0) hit = hot_run(pool, hdesc + 8 * h, t0, e, e + wa < L ? e + wa : L);
+                    if (hit) hot |= 1u << h;
+                }
+            }
+            pres[i].lik = (int16_t)lik;
+            phot[i] = hot;
+        }
+    }
+}
+
+// per scan lane: finditer skipping per pattern over the lane's matched pairs (variant independent),
+// then the validator-passing survivors become the rows' resident candidates (wc, in pair-queue slots
+// of the lane: a lane never has more candidates than pairs)
+__global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
+                                                   const uint32_t* __restrict__ lane_np,
+                                                   const EvLoc* __restrict__ evloc, const PairRes* __restrict__ pres,
+                                                   const int32_t* __restrict__ pend, const uint32_t* __restrict__ phot,
+                                                   uint64_t pair_cap, int n_pat, WCand* __restrict__ wc,
+                                                   uint32_t* __restrict__ wc_first, uint32_t* __restrict__ wc_n,
+                                                   const uint32_t* __restrict__ err) {
+    if (*err & ERR_QUEUE) return;
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    const uint32_t np = lane_np[c];
+    const uint64_t base = lane_pair[c];
+    if (np == 0 || base + np > pair_cap) return;
+    uint32_t u = 0xffffffffu, k = 0, uf = 0;
+    int lp[LIVE], le[LIVE];
+    uint32_t cur_s[P_MAX];
+    bool spilled = false;
+#pragma unroll
+    for (int q = 0; q < LIVE; ++q) {
+        lp[q] = -1;
+        le[q] = -1;
+    }
+    for (uint32_t i = 0; i < np; ++i) {
+        const int e = pend[base + i];
+        if (e < 0) continue;
+        const PairRes P = pres[base + i];
+        const EvLoc Lc = evloc[P.ev];
+        const int s = (int)(Lc.s - Lc.ustart);
+        if (Lc.u != u) {
+            if (u != 0xffffffffu && k > uf) {
+                wc_first[u] = (uint32_t)(base + uf);
+                wc_n[u] = k - uf;
+            }
+            u = Lc.u;
+            uf = k;
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q) {
+                lp[q] = -1;
+                le[q] = -1;
+            }
+            spilled = false;
+        }
+        const int p = P.p;
+        int prev_end = -1;
+        if (spilled) {
+            prev_end = (int)cur_s[p];
+        } else {
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q)
+                if (lp[q] == p) prev_end = le[q];
+        }
+        if (s < prev_end) continue;                    // inside p's previous match (finditer)
+        if (spilled) {
+            cur_s[p] = (uint32_t)e;
+        } else {
+            int slot = -1;
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q)
+                if (lp[q] == p) slot = q;
+            if (slot < 0) {
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q)
+                    if (slot < 0 && le[q] <= s) slot = q;
+            }
+            if (slot >= 0) {
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q)
+                    if (q == slot) {
+                        lp[q] = p;
+                        le[q] = e;
+                    }
+            } else {
+                for (int q = 0; q < n_pat; ++q) cur_s[q] = 0;
+#pragma unroll
+                for (int q = 0; q < LIVE; ++q)
+                    if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
+                cur_s[p] = (uint32_t)e;
+                spilled = true;
+            }
+        }
+        if (P.lik < 0) continue;                       // validator failed
+        WCand C;
+        C.s = (uint32_t)s;
+        C.e = (uint32_t)e;
+        C.p = (uint16_t)p;
+        C.pad = 0;
+        C.hot = phot[base + i];
+        wc[base + k++] = C;
+    }
+    if (u != 0xffffffffu && k > uf) {
+        wc_first[u] = (uint32_t)(base + uf);
+        wc_n[u] = k - uf;
+    }
+}
+
+// per row: upper bound of its window's findings (= candidates in the window) for the findings arena;
+// clears the row's ring-commit plan
+__global__ __launch_bounds__(256) void k_win_plan(const WinRing W, const WinBatch B, uint32_t* __restrict__ bound,
+                                                  WNew* __restrict__ wnew, const uint32_t* __restrict__ err) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= B.n_utt) return;
+    WNew z;
+    z.off = 0xffffffffu;
+    z.ri = z.cnt = z.head = 0;
+    wnew[u] = z;
+    if (*err & (ERR_QUEUE | ERR_SLOT)) {
+        bound[u] = 0;
+        return;
+    }
+    WEntry E[WN_MAX];
+    const int nw = win_entries(W, B, u, E);
+    uint32_t b = 0;
+    for (int j = 0; j < nw; ++j) b += E[j].nc;
+    bound[u] = b;
+}
+
+// per window: the window's context variant -> hotword likelihoods (resident bits, or a re-run over
+// the halo when a proximity window crosses a '\n'), min likelihood, exclusion, overlap; findings in
+// window coordinates, output length
+__global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
+                                                    const WinRing W, const WinBatch B,
+                                                    const int16_t* __restrict__ win_ctx,
+                                                    const uint64_t* __restrict__ fbase, uint64_t fcap,
+                                                    pii_span* __restrict__ wfd, uint32_t* __restrict__ n_wfind,
+                                                    uint32_t* __restrict__ wout_len, uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    if (*err & (ERR_QUEUE | ERR_SLOT)) return;
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[WS_TRANS]), lb + li.off[WS_CMAP]};
+    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[WS_HDESC]);
+    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[WS_HRULE]);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[WS_DTYPE]);
+    const uint8_t* dlik = lb + li.off[WS_DLIK];
+    const uint8_t* ven = lb + li.off[WS_VEN];
+    const uint8_t* vmin = lb + li.off[WS_VMIN];
+    const uint8_t* dex = lb + li.off[WS_DEX];
+    const uint32_t* xoff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_XOFF]);
+    const uint16_t* xids = reinterpret_cast<const uint16_t*>(lb + li.off[WS_XIDS]);
+    const uint32_t* tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_TOKOFF]);
+    const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_ROFF]);
+    const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + li.off[WS_RIDS]);
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= B.n_utt) return;
+    if (fbase[B.n_utt] > fcap) {                  // findings arena too small: re-run with the exact size
+        if (u == 0) atomicOr(err, (uint32_t)ERR_QUEUE);
+        return;
+    }
+    WEntry E[WN_MAX];
+    uint32_t O[WN_MAX];
+    const int nw = win_entries(W, B, u, E);
+    uint32_t o = 0;
+    for (int j = 0; j < nw; ++j) {
+        O[j] = o;
+        o += E[j].len + 1;
+    }
+    const uint32_t WL = o - 1;
+    const int T = R.T;
+    const int g = win_ctx[u];
+    const int v = g >= 0 ? g + 1 : 0;
+    const int minlik = vmin[v];
+    pii_span* fdu = wfd + fbase[u];
+    uint32_t nf = 0;
+    int delta = 0;
+    uint32_t max_end = 0;
+    for (int j = 0; j < nw; ++j) {
+        const WEntry Ej = E[j];
+        const uint32_t oj = O[j];
+        int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
+        uint32_t ex_valid = 0;
+        int s = -1, best_e = -1, best_t = 0, best_lik = 0;
+        auto flush_start = [&]() {
+            if (best_e >= 0 && oj + (uint32_t)s >= max_end) {
+                pii_span f;
+                f.utt = u;
+                f.start = oj + (uint32_t)s;
+                f.end = oj + (uint32_t)best_e;
+                f.info_type = (uint16_t)best_t;
+                f.likelihood = (uint8_t)best_lik;
+                f.flags = 0;
+                fdu[nf++] = f;
+                max_end = f.end;
+                delta += (int)(tokoff[best_t + 1] - tokoff[best_t]) - (best_e - s);
+            }
+            best_e = -1;
+        };
+        for (uint32_t k = 0; k < Ej.nc; ++k) {
+            const WCand C = Ej.c[k];
+            const int cs = (int)C.s, e = (int)C.e;
+            if (cs != s) {
+                flush_start();
+                s = cs;
+            }
+            const int p = C.p;
+            const int t = dtype[p];
+            if (!ven[v * T + t]) continue;
+            int lik = dlik[p];
+            const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
+            for (uint32_t q = r0; q < r1; ++q) {
+                const int h = rids[q];
+                const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
+                const bool cb = wb > 0 && s < wb && j > 0;                       // reaches the previous utterance
+                const bool ca = wa > 0 && (uint32_t)(e + wa) > Ej.len && j + 1 < nw;   // reaches the next one
+                bool hit;
+                if (h < 32 && ((C.hot >> h) & 1u)) {
+                    hit = true;                                                 // inside the utterance
+                } else if (h < 32 && !cb && !ca) {
+                    hit = false;
+                } else {
+                    const uint32_t ps = oj + (uint32_t)s, pe = oj + (uint32_t)e;
+                    hit = wb > 0 && hot_run_win(pool, hdesc + 8 * h, E, O, nw, ps > (uint32_t)wb ? ps - wb : 0u, ps);
+                    if (!hit && wa > 0) hit = hot_run_win(pool, hdesc + 8 * h, E, O, nw, pe, min(WL, pe + (uint32_t)wa));
+                }
+                if (hit) {
+                    const int fixed = hrule[4 * h + 2], rel = hrule[4 * h + 3];
+                    if (fixed) {
+                        lik = fixed;
+                    } else {
+                        lik += rel;
+                        lik = lik < 1 ? 1 : (lik > 5 ? 5 : lik);
+                    }
+                }
+            }
+            const int xi = dex[p];
+            if (lik < minlik) {
+                if (xi != 0xff) ex_valid &= ~(1u << xi);
+                continue;
+            }
+            if (xi != 0xff) {
+#pragma unroll
+                for (int x = 0; x < NE_MAX; ++x)
+                    if (x == xi) {
+                        ex_s[x] = s;
+                        ex_e[x] = e;
+                        ex_t[x] = t;
+                    }
+                ex_valid |= 1u << xi;
+            }
+            const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
+            bool excluded = false;
+            for (uint32_t q = x0; q < x1; ++q) {
+                const int xt = xids[q];
+#pragma unroll
+                for (int x = 0; x < NE_MAX; ++x)
+                    if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
+                        excluded = true;
+            }
+            if (excluded) continue;
+            const bool better = best_e < 0 || e > best_e ||
+                                (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
+            if (better) {
+                best_e = e;
+                best_t = t;
+                best_lik = lik;
+            }
+        }
+        flush_start();
+    }
+    n_wfind[u] = nf;
+    wout_len[u] = (uint32_t)((int)WL + delta);
+}
+
+// per conversation run (its last row): place the run's newest min(N, run) rows in the history ring.
+// Entries are contiguous in the slot's arena (wrap to 0 when the tail is short); the final live set
+// must not overlap, else ERR_RING (raise slot_bytes).  Nothing is written to the ring here.
+__global__ __launch_bounds__(256) void k_win_alloc(const WinRing W, const WinBatch B, WNew* __restrict__ wnew,
+                                                   uint32_t* __restrict__ err) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= B.n_utt || (*err & (ERR_QUEUE | ERR_SLOT))) return;
+    const uint32_t sl = B.slot[u];
+    if (sl >= W.n_slots || (u + 1 < B.n_utt && B.slot[u + 1] == sl)) return;
+    uint32_t k = 1;
+    while (k < W.N && u >= k && B.slot[u - k] == sl) ++k;
+    const uint32_t cnt = W.cnt[sl], head = W.head[sl], N = W.N, cap = W.slot_bytes;
+    const uint32_t keep = min(cnt, N - k);                 // old entries that stay live
+    uint32_t lo[WN_MAX], hi[WN_MAX];
+    int nl = 0;
+    uint32_t end = 0;
+    for (uint32_t i = 0; i < cnt; ++i) {                    // oldest live .. newest
+        const WDesc D = W.desc[(size_t)sl * N + (head + N - cnt + i) % N];
+        end = D.off + 16u * D.nc + ((D.len + 15u) & ~15u);
+        if (i >= cnt - keep) {
+            lo[nl] = D.off;
+            hi[nl] = end;
+            ++nl;
+        }
+    }
+    bool bad = false;
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t v = u - k + 1 + i;
+        const uint64_t size = 16ull * B.wc_n[v] + ((B.offs[v + 1] - B.offs[v] + 15) & ~15ull);
+        if (size > cap) {
+            bad = true;
+            break;
+        }
+        uint32_t pos = end;
+        if ((uint64_t)pos + size > cap) pos = 0;
+        for (int q = 0; q < nl; ++q)
+            if (pos < hi[q] && lo[q] < pos + (uint32_t)size) bad = true;
+        lo[nl] = pos;
+        hi[nl] = pos + (uint32_t)size;
+        ++nl;
+        end = pos + (uint32_t)size;
+        WNew w;
+        w.off = pos;
+        w.ri = (head + i) % N;
+        w.cnt = min(N, cnt + k);
+        w.head = (head + k) % N;
+        wnew[v] = w;
+    }
+    if (bad) atomicOr(err, (uint32_t)ERR_RING);
+}
+
+// window output byte `rel` (slow path for windows whose pieces overflow the tile's LDS table)
+__device__ uint8_t win_byte_slow(const RulesDev& R, const WEntry* E, const uint32_t* O, int nw,
+                                 const pii_span* F, uint32_t nf, uint32_t rel) {
+    uint32_t pout = 0, fi = 0;
+    for (int j = 0; j < nw; ++j) {
+        const uint32_t sh = O[j] + E[j].len;
+        uint32_t pin = O[j];
+        while (fi < nf && F[fi].start < sh) {
+            const uint32_t run = F[fi].start - pin;
+            if (rel < pout + run) return E[j].t[pin - O[j] + (rel - pout)];
+            pout += run;
+            const uint32_t t0 = R.tok_off[F[fi].info_type], tl = R.tok_off[F[fi].info_type + 1] - t0;
+            if (rel < pout + tl) return R.tok_bytes[t0 + (rel - pout)];
+            pout += tl;
+            pin = F[fi].end;
+            ++fi;
+        }
+        const uint32_t run = sh - pin;
+        if (rel < pout + run) return E[j].t[pin - O[j] + (rel - pout)];
+        pout += run;
+        if (rel == pout) return '\n';
+        ++pout;
+    }
+    return 0;
+}
+
+// WIN_TILE windows per workgroup: piece table (copy runs of each resident / batch utterance, tokens,
+// '\n' separators) in LDS, then the shared 16-byte block assembly; spans copied out
+__global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, const WinRing W, const WinBatch B,
+                                                             const pii_span* __restrict__ wfd,
+                                                             const uint64_t* __restrict__ fbase,
+                                                             const uint32_t* __restrict__ n_wfind,
+                                                             const uint64_t* __restrict__ out_offs,
+                                                             const uint64_t* __restrict__ span_offs,
+                                                             const uint32_t* __restrict__ err, uint8_t* __restrict__ out,
+                                                             pii_span* __restrict__ spans) {
+    __shared__ uint32_t s_pout[PIECE_MAX + 1];
+    __shared__ uint64_t s_psrc[PIECE_MAX + 1];
+    __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
+    __shared__ uint16_t s_bp[BLK_MAX];
+    __shared__ uint32_t s_total;
+    if (*err != 0) return;
+    const uint32_t u0 = blockIdx.x * WIN_TILE;
+    const uint32_t u1 = min(u0 + WIN_TILE, B.n_utt);
+    const uint32_t nu = u1 - u0;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t out_lo = (int64_t)out_offs[u0], out_hi = (int64_t)out_offs[u1];
+    const bool mine = (uint32_t)tid < nu;        // WIN_TILE == 64: wavefront 0 owns the windows
+    const uint32_t u = u0 + tid;
+    WEntry E[WN_MAX];
+    uint32_t O[WN_MAX];
+    int nw = 0;
+    uint32_t nf = 0;
+    if (mine) {
+        nw = win_entries(W, B, u, E);
+        uint32_t o = 0;
+        for (int j = 0; j < nw; ++j) {
+            O[j] = o;
+            o += E[j].len + 1;
+        }
+        nf = n_wfind[u];
+    }
+    const uint32_t cnt = mine ? 2 * nf + 2 * (uint32_t)nw - 1 : 0;
+    uint32_t incl = cnt;
+    if (wid == 0) {
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        if (lane == 63) s_total = incl;
+    }
+    __syncthreads();
+    const uint32_t total_p = s_total;
+    const bool staged = total_p <= PIECE_MAX;
+    if (mine) {
+        const pii_span* F = wfd + fbase[u];
+        pii_span* sp = spans + span_offs[u];
+        for (uint32_t f = 0; f < nf; ++f) sp[f] = F[f];
+        if (staged) {
+            uint32_t pb = incl - cnt;
+            uint32_t po = (uint32_t)((int64_t)out_offs[u] - out_lo);
+            uint32_t fi = 0;
+            for (int j = 0; j < nw; ++j) {
+                const uint32_t sh = O[j] + E[j].len;
+                const uint64_t src = (uint64_t)(uintptr_t)E[j].t - O[j];     // window position -> address
+                uint32_t pin = O[j];
+                while (fi < nf && F[fi].start < sh) {
+                    const pii_span Fi = F[fi];
+                    s_pout[pb] = po;
+                    s_psrc[pb] = src + pin;
+                    ++pb;
+                    po += Fi.start - pin;
+                    const uint32_t t0 = R.tok_off[Fi.info_type];
+                    s_pout[pb] = po;
+                    s_psrc[pb] = (uint64_t)(uintptr_t)(R.tok_bytes + t0);
+                    ++pb;
+                    po += R.tok_off[Fi.info_type + 1] - t0;
+                    pin = Fi.end;
+                    ++fi;
+                }
+                s_pout[pb] = po;
+                s_psrc[pb] = src + pin;
+                ++pb;
+                po += sh - pin;
+                if (j + 1 < nw) {
+                    s_pout[pb] = po;
+                    s_psrc[pb] = (uint64_t)(uintptr_t)(R.tok_bytes + R.nl_off);
+                    ++pb;
+                    po += 1;
+                }
+            }
+        }
+    }
+    if (tid == 0 && staged) s_pout[total_p] = (uint32_t)(out_hi - out_lo);
+    __syncthreads();
+    if (staged) {
+        tile_assemble(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
+    } else {
+        // one window at a time per wavefront, byte-granular (wavefront 0 holds the entry lists)
+        if (wid == 0) {
+            for (uint32_t i = 0; i < nu; ++i) {
+                const uint32_t uu = u0 + i;
+                WEntry Ei[WN_MAX];
+                uint32_t Oi[WN_MAX];
+                const int nwi = win_entries(W, B, uu, Ei);
+                uint32_t o = 0;
+                for (int j = 0; j < nwi; ++j) {
+                    Oi[j] = o;
+                    o += Ei[j].len + 1;
+                }
+                const pii_span* F = wfd + fbase[uu];
+                const uint32_t nfi = n_wfind[uu];
+                uint8_t* dst = out + out_offs[uu];
+                const uint32_t olen = (uint32_t)(out_offs[uu + 1] - out_offs[uu]);
+                for (uint32_t rel = lane; rel < olen; rel += 64) dst[rel] = win_byte_slow(R, Ei, Oi, nwi, F, nfi, rel);
+            }
+        }
+    }
+}
+
+// after a successful call: the planned rows enter the rings (16 threads per row copy the resident
+// candidates, then the text, as aligned 16-byte stores); descriptors, counts and heads follow
+__global__ __launch_bounds__(256) void k_win_commit(const WinRing W, const WinBatch B, const WNew* __restrict__ wnew,
+                                                    const uint32_t* __restrict__ err) {
+    if (*err != 0) return;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t v = (uint32_t)(gid >> 4), t = (uint32_t)(gid & 15);
+    if (v >= B.n_utt) return;
+    const WNew w = wnew[v];
+    if (w.off == 0xffffffffu) return;
+    const uint32_t sl = B.slot[v];
+    const uint32_t nc = B.wc_n[v];
+    const uint64_t a = B.offs[v];
+    const uint32_t len = (uint32_t)(B.offs[v + 1] - a);
+    uint8_t* dst = W.arena + (size_t)sl * W.slot_bytes + w.off;
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    if (nc) {
+        const uint4* c4 = reinterpret_cast<const uint4*>(B.wc + B.wc_first[v]);
+        for (uint32_t k = t; k < nc; k += 16) d4[k] = c4[k];
+    }
+    const uint8_t* src = B.text + a;
+    for (uint32_t q = t; 16 * q < len; q += 16) {
+        const int n = len - 16 * q < 16 ? (int)(len - 16 * q) : 16;
+        d4[nc + q] = load16(src + 16 * q, 0, n);
+    }
+    if (t == 0) {
+        WDesc D;
+        D.off = w.off;
+        D.len = len;
+        D.nc = nc;
+        D.pad = 0;
+        W.desc[(size_t)sl * W.N + w.ri] = D;
+        const bool last = v + 1 == B.n_utt || B.slot[v + 1] != sl;
+        if (last) {
+            W.cnt[sl] = w.cnt;
+            W.head[sl] = w.head;
+        }
     }
 }
 
@@ -1498,7 +2195,7 @@ struct pii_engine {
     uint32_t n_slots = 0;
     int64_t ttl_us = 0;
     size_t scan_lds = 0;
-    DevImage img_first, img_eval, img_sel;     // per-kernel LDS images of the rule tables
+    DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
     int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
@@ -1567,6 +2264,23 @@ struct pii_engine {
     hipEvent_t kev[4] = {};           // around k_scan and k_redact (the roofline kernels)
     bool kev_valid = false;
     float last_kms[2] = {};
+    int last_kind = 0;                // 0 = pii_scan_redact*, 1 = pii_rescan_window* (what pii_sync re-runs)
+    // window re-scan (a12): resident history rings + per-call scratch
+    uint32_t win_n = 0, win_slot_bytes = 0;
+    bool window_ok = false;
+    WDesc* wr_desc = nullptr;
+    uint32_t *wr_cnt = nullptr, *wr_head = nullptr;
+    uint8_t* wr_arena = nullptr;
+    WCand* wc = nullptr;
+    uint32_t* phot = nullptr;
+    uint64_t wc_cap = 0;
+    uint32_t *wc_first = nullptr, *wc_n = nullptr, *wbound = nullptr, *n_wfind = nullptr, *wout_len = nullptr;
+    uint64_t *wfbase = nullptr, *wspan_offs = nullptr;
+    WNew* wnew = nullptr;
+    int16_t* wctx = nullptr;
+    uint32_t wcap_utt = 0;
+    pii_span* wfd = nullptr;
+    uint64_t wfd_cap = 0;
 };
 
 #define HIPCHK(x)                                                                  \
@@ -1659,15 +2373,9 @@ int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out,
     return PII_OK;
 }
 
-int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
-                 const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
-                 uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info, hipStream_t st) {
-    if (total_bytes > PII_MAX_BATCH_BYTES) {
-        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
-        return PII_E_ARG;
-    }
-    int rc = ensure_scratch(e, n_utt, total_bytes);
-    if (rc) return rc;
+// queues sized for a batch of `total_bytes`
+int ensure_queues(pii_engine* e, uint64_t total_bytes) {
+    int rc;
     if (e->pair_cap < total_bytes / 16 + 4096) {
         const uint64_t cap = total_bytes / 16 + 4096;
         if ((rc = grow_pairs(e, cap))) return rc;
@@ -1678,22 +2386,23 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         if ((rc = grow(e, e->evloc, cap)) || (rc = grow(e, e->evpairs, cap))) return rc;
         e->ev_cap = cap;
     }
-    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
-                               ctx_info, st};
+    return PII_OK;
+}
+
+// The stages every call shares: lane index, reverse DFA scan, (start, pattern) pair queue, context
+// (segmented scan), leftmost-first confirmation.  Records tev[0..2].
+int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint32_t n_chunks,
+                 const uint32_t* slot, const uint8_t* role, const int64_t* ts, int16_t* ctx, int16_t* win_ctx,
+                 const unsigned long long* pcount, hipStream_t st) {
     const RulesDev& R = e->R;
-    int16_t* ctx = ctx_info ? ctx_info : e->ctx;
     e->epoch += 1;
     HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), st));
     HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
-    e->kev_valid = n_utt > 0 && total_bytes > 0;
     HIPCHK(hipEventRecord(e->tev[0], st));
-    const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
-    // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
-    const unsigned long long* pcount =
-        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, R.kw_always_min,
-                                                                e->first_utt, e->out_len, e->n_find, e->kw);
+                                                                e->first_utt, e->out_len, e->n_find, e->kw,
+                                                                win_ctx ? e->wc_n : nullptr);
         if (n_chunks > 0) {
             k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(offs, e->first_utt, n_chunks,
                                                                 (int64_t)((uintptr_t)text & 63), e->bnd);
@@ -1705,6 +2414,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
                                                         e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
                                                         e->lane_pair, e->lane_ev, e->lane_np, e->d_err);
+            int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
             if ((rc = exclusive_scan(e, e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
             k_pairs<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
@@ -1721,7 +2431,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                e->stamp, e->epoch, e->d_err);
         k_ctx_apply<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, role, e->kw, ts, n_utt, e->n_slots, e->ttl_us,
                                                          e->incl, e->agg_v, e->agg_f, e->st_group, e->st_ts, ctx,
-                                                         e->commit);
+                                                         e->commit, win_ctx);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
@@ -1729,6 +2439,32 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         k_pair_first<<<e->n_seg, PAIR_BLOCK, e->img_first.li.total, st>>>(
             e->img_first.d, e->img_first.li, text, offs, pcount, e->pair_cap, e->evloc, e->pres, e->pend, e->matched,
             e->cont, e->mcount, e->d_err);
+        HIPCHK(hipGetLastError());
+    }
+    return PII_OK;
+}
+
+int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
+                 const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
+                 uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info, hipStream_t st) {
+    if (total_bytes > PII_MAX_BATCH_BYTES) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
+        return PII_E_ARG;
+    }
+    int rc = ensure_scratch(e, n_utt, total_bytes);
+    if (rc || (rc = ensure_queues(e, total_bytes))) return rc;
+    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
+                               ctx_info, st};
+    e->last_kind = 0;
+    const RulesDev& R = e->R;
+    int16_t* ctx = ctx_info ? ctx_info : e->ctx;
+    e->kev_valid = n_utt > 0 && total_bytes > 0;
+    const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
+    // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
+    const unsigned long long* pcount =
+        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, slot, role, ts, ctx, nullptr, pcount, st))) return rc;
+    if (n_utt > 0 && n_chunks > 0) {
         k_pair_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
             e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
             e->mcount, e->n_seg, e->evloc, e->pend, e->pres);
@@ -1741,7 +2477,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
     if ((rc = exclusive_scan(e, e->n_find, n_utt, e->span_offs, st))) return rc;
     k_finalize<<<1, 1, 0, st>>>(out_offs, e->span_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
-                                pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr);
+                                pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
@@ -1758,11 +2494,114 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
-    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(e->tev[6], st));
     return PII_OK;
 }
 
+int ensure_window_scratch(pii_engine* e, uint32_t n_utt) {
+    int rc;
+    if (e->wc_cap < e->pair_cap) {
+        if ((rc = grow(e, e->wc, e->pair_cap)) || (rc = grow(e, e->phot, e->pair_cap))) return rc;
+        e->wc_cap = e->pair_cap;
+    }
+    if (n_utt > e->wcap_utt) {
+        const uint32_t nu = std::max<uint32_t>(n_utt + n_utt / 8, 1024);
+        if ((rc = grow(e, e->wc_first, nu)) || (rc = grow(e, e->wc_n, nu)) || (rc = grow(e, e->wbound, nu)) ||
+            (rc = grow(e, e->wfbase, (size_t)nu + 1)) || (rc = grow(e, e->n_wfind, nu)) ||
+            (rc = grow(e, e->wout_len, nu)) || (rc = grow(e, e->wnew, nu)) || (rc = grow(e, e->wctx, nu)) ||
+            (rc = grow(e, e->wspan_offs, (size_t)nu + 1)))
+            return rc;
+        e->wcap_utt = nu;
+    }
+    const uint64_t want = std::max<uint64_t>(4096, 4ull * n_utt);
+    if (e->wfd_cap < want) {
+        if ((rc = grow(e, e->wfd, want))) return rc;
+        e->wfd_cap = want;
+    }
+    return PII_OK;
+}
+
+// the window re-scan call (a12): the shared front over the NEW rows only, then resident candidates,
+// window selection, window redaction, ring commit
+int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
+               const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
+               uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* win_ctx, hipStream_t st) {
+    if (e->win_n == 0) {
+        e->err = "window re-scan not enabled (pii_window_enable)";
+        return PII_E_ARG;
+    }
+    if (total_bytes > PII_MAX_BATCH_BYTES) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
+        return PII_E_ARG;
+    }
+    int rc = ensure_scratch(e, n_utt, total_bytes);
+    if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_window_scratch(e, n_utt))) return rc;
+    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
+                               win_ctx, st};
+    e->last_kind = 1;
+    const RulesDev& R = e->R;
+    int16_t* wctx = win_ctx ? win_ctx : e->wctx;
+    e->kev_valid = n_utt > 0 && total_bytes > 0;
+    const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
+    const unsigned long long* pcount =
+        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, slot, role, ts, e->ctx, wctx, pcount, st))) return rc;
+    if (n_utt > 0 && n_chunks > 0) {
+        k_win_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
+            e->img_eval.d, e->img_eval.li, text, offs, pcount, e->pair_cap, e->matched, e->mcount, e->n_seg,
+            e->evloc, e->pend, e->pres, e->phot);
+        k_win_cands<<<(n_chunks + 255) / 256, 256, 0, st>>>(n_chunks, e->lane_pair, e->lane_np, e->evloc, e->pres,
+                                                            e->pend, e->phot, e->pair_cap, R.P, e->wc, e->wc_first,
+                                                            e->wc_n, e->d_err);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(e->tev[3], st));
+    const WinRing W{e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->win_n, e->win_slot_bytes, e->n_slots, 0};
+    const WinBatch B{text, offs, slot, e->wc, e->wc_first, e->wc_n, n_utt};
+    const uint32_t nb = (n_utt + 255) / 256;
+    if (n_utt > 0) {
+        k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
+        if ((rc = exclusive_scan(e, e->wbound, n_utt, e->wfbase, st))) return rc;
+        k_win_select<<<nb, 256, e->img_wsel.li.total, st>>>(R, e->img_wsel.d, e->img_wsel.li, W, B, wctx, e->wfbase,
+                                                             e->wfd_cap, e->wfd, e->n_wfind, e->wout_len, e->d_err);
+        HIPCHK(hipGetLastError());
+    }
+    if ((rc = exclusive_scan(e, e->wout_len, n_utt, out_offs, st))) return rc;
+    if ((rc = exclusive_scan(e, e->n_wfind, n_utt, e->wspan_offs, st))) return rc;
+    if (n_utt > 0) k_win_alloc<<<nb, 256, 0, st>>>(W, B, e->wnew, e->d_err);
+    k_finalize<<<1, 1, 0, st>>>(out_offs, e->wspan_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
+                                pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, n_utt > 0 ? e->wfbase + n_utt : nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->tev[4], st));
+    if (n_utt > 0) {
+        HIPCHK(hipEventRecord(e->kev[2], st));
+        k_win_redact<<<(n_utt + WIN_TILE - 1) / WIN_TILE, REDACT_BLOCK, 0, st>>>(
+            R, W, B, e->wfd, e->wfbase, e->n_wfind, out_offs, e->wspan_offs, e->d_err, out, spans);
+        HIPCHK(hipEventRecord(e->kev[3], st));
+        k_win_commit<<<(uint32_t)(((uint64_t)n_utt * 16 + 255) / 256), 256, 0, st>>>(W, B, e->wnew, e->d_err);
+        k_ctx_commit<<<nb, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err, e->st_group,
+                                         e->st_ts);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(e->tev[5], st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(e->tev[6], st));
+    return PII_OK;
+}
+
+int rerun_last(pii_engine* e) {
+    const pii_engine::Call c = e->last;
+    if (e->last_kind == 1)
+        return run_window(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
+                          c.spans, c.span_cap, c.ctx_info, c.st);
+    return run_pipeline(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
+                        c.spans, c.span_cap, c.ctx_info, c.st);
+}
+
+int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
+                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream);
 }  // namespace
 
 extern "C" {
@@ -1806,6 +2645,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.k_start = (int)meta[9];
     R.n_hot = (int)meta[10];
     R.min_len = (int)std::max<int64_t>(1, meta[11]);
+    e->window_ok = meta[13] != 0;
     auto fail = [&](const char* why) {
         e->err = why;
         pii_engine_destroy(e);
@@ -1888,6 +2728,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         tok += "[" + e->names[t] + "]";
         tok_off[t + 1] = (uint32_t)tok.size();
     }
+    tok += "\n";               // the re-scan window separator (k_win_redact piece source)
+    R.nl_off = (uint32_t)tok.size() - 1;
     tok.append(32, '\0');     // k_redact reads aligned 16-byte windows past a token's end
     // one device buffer holding every table, 256-byte aligned sections
     struct Put {
@@ -1970,6 +2812,33 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         pe[EV_DLIK] = sec("det.lik");
         pe[EV_ROFF] = sec("var.rule_off");
         pe[EV_RIDS] = sec("var.rule_ids");
+        // per type: every hotword rule it has in any context variant (k_win_eval's resident bits)
+        std::vector<uint32_t> thot(std::max(R.T, 1), 0u);
+        {
+            const uint32_t* ro = (const uint32_t*)find("var.rule_off")->data;
+            const uint16_t* ri = (const uint16_t*)find("var.rule_ids")->data;
+            for (int v = 0; v < R.V; ++v)
+                for (int t = 0; t < R.T; ++t)
+                    for (uint32_t q = ro[v * R.T + t]; q < ro[v * R.T + t + 1]; ++q)
+                        if (ri[q] < 32) thot[t] |= 1u << ri[q];
+        }
+        pe[EV_THOT] = vec(thot);
+        std::vector<std::pair<const void*, size_t>> pw(WS_N);
+        pw[WS_TRANS] = vec(hp.trans);
+        pw[WS_CMAP] = vec(hp.cmap);
+        pw[WS_HDESC] = vec(hp.desc);
+        pw[WS_HRULE] = sec("hot.rule");
+        pw[WS_DTYPE] = sec("det.type");
+        pw[WS_DLIK] = sec("det.lik");
+        pw[WS_VEN] = sec("var.enabled");
+        pw[WS_VMIN] = sec("var.minlik");
+        pw[WS_DEX] = sec("det.exidx");
+        pw[WS_XOFF] = sec("var.excl_off");
+        pw[WS_XIDS] = sec("var.excl_ids");
+        pw[WS_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
+        pw[WS_ROFF] = sec("var.rule_off");
+        pw[WS_RIDS] = sec("var.rule_ids");
+        if (!make_image(pw, e->img_wsel)) return fail("rule tables do not fit in LDS / upload failed");
         ps[SE_DTYPE] = sec("det.type");
         ps[SE_VEN] = sec("var.enabled");
         ps[SE_VMIN] = sec("var.minlik");
@@ -1981,7 +2850,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("rule tables do not fit in LDS / upload failed");
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first, &e->img_first}, {(const void*)k_pair_eval, &e->img_eval},
-            {(const void*)k_select, &e->img_sel}};
+            {(const void*)k_select, &e->img_sel}, {(const void*)k_win_eval, &e->img_eval},
+            {(const void*)k_win_select, &e->img_wsel}};
         for (auto& kb : big)
             if (kb.second->li.total > 64 * 1024 &&
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
@@ -2029,7 +2899,9 @@ int pii_engine_destroy(pii_engine* e) {
                     e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->d_err, e->d_totals, e->h_text, e->h_role,
-                    e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx};
+                    e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
+                    e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
+                    e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
@@ -2075,26 +2947,18 @@ int pii_scan_redact_device(pii_engine* e, const uint8_t* d_bytes, const uint64_t
                            const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out,
                            uint64_t out_cap, uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
                            int16_t* d_ctx_info, void* stream) {
-    if (!e || !d_offsets || !d_slot || !d_role || !d_out_offsets) return PII_E_ARG;
-    if (n_utt > 0 && (!d_bytes || !d_out || !d_spans)) return PII_E_ARG;
-    HIPCHK(hipSetDevice(e->device));
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
-    uint64_t tb[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(tb, d_offsets, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(tb + 1, d_offsets + n_utt, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (tb[1] < tb[0]) return PII_E_ARG;
-    return run_pipeline(e, d_bytes, d_offsets, n_utt, tb[1] - tb[0], d_slot, d_role, d_ts, d_out, out_cap,
-                        d_out_offsets, d_spans, span_cap, d_ctx_info, st);
+    return device_call(e, false, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,
+                       d_spans, span_cap, d_ctx_info, stream);
 }
 
 int pii_sync(pii_engine* e, uint64_t totals[3]) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipEventSynchronize(e->tev[6]));
     for (int attempt = 0; (e->h_totals[2] & ERR_QUEUE) && attempt < 4; ++attempt) {
-        // the (start, pattern) pair queue overflowed: grow it to the exact need and run the batch again
-        // (the conversation context was not committed, so the re-run is idempotent)
-        const uint64_t need = e->h_totals[3] + 4096, need_ev = e->h_totals[4] + 4096;
+        // a work queue overflowed (pair queue, event records, window findings): grow it to the exact
+        // need and run the batch again (context and window history were not committed, so the re-run
+        // is idempotent)
+        const uint64_t need = e->h_totals[3] + 4096, need_ev = e->h_totals[4] + 4096, need_wf = e->h_totals[5] + 4096;
         if (need_ev > e->ev_cap) {
             int rc = grow(e, e->evloc, need_ev);
             if (!rc) rc = grow(e, e->evpairs, need_ev);
@@ -2104,11 +2968,11 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         int rc = grow_pairs(e, std::max(need, e->pair_cap));
         if (rc) return rc;
         e->pair_cap = std::max(need, e->pair_cap);
-        const pii_engine::Call c = e->last;
-        e->epoch += 0;
-        rc = run_pipeline(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
-                          c.spans, c.span_cap, c.ctx_info, c.st);
-        if (rc) return rc;
+        if (e->last_kind == 1 && need_wf > e->wfd_cap) {
+            if ((rc = grow(e, e->wfd, need_wf))) return rc;
+            e->wfd_cap = need_wf;
+        }
+        if ((rc = rerun_last(e))) return rc;
         HIPCHK(hipEventSynchronize(e->tev[6]));
     }
     float tot = 0;
@@ -2131,6 +2995,10 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
     }
     const uint64_t f = e->h_totals[2];
     if (f & ERR_SLOT) return PII_E_ARG;
+    if (f & ERR_RING) {
+        e->err = "a conversation's re-scan window does not fit its history slot; raise slot_bytes (pii_window_enable)";
+        return PII_E_NOMEM;
+    }
     if (f & ERR_ORDER) return PII_E_ORDER;
     if (f & ERR_QUEUE) return PII_E_NOMEM;
     if (f & ERR_CAPACITY) return PII_E_CAPACITY;
@@ -2160,10 +3028,14 @@ int pii_last_timings_ex(pii_engine* e, float* ms, uint32_t n) {
     return (int)std::min<uint32_t>(n, 8);
 }
 
-int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
-                    const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
-                    uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
-                    int16_t* ctx_info) {
+}  // extern "C"
+
+namespace {
+// host-buffer calls: stage the rows through the engine's device buffers, run, wait, copy back
+int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+              const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
+              uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
+              int16_t* ctx_info) {
     if (!e || !offsets || !out_offsets || (n_utt && (!conv_slot || !role))) return PII_E_ARG;
     for (uint32_t i = 0; i < n_utt; ++i)
         if (offsets[i + 1] < offsets[i]) return PII_E_ARG;
@@ -2203,8 +3075,9 @@ int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets
         HIPCHK(hipMemcpyAsync(e->h_role, role, n_utt, hipMemcpyHostToDevice, st));
         if (ts_us) HIPCHK(hipMemcpyAsync(e->h_ts, ts_us, n_utt * 8, hipMemcpyHostToDevice, st));
     }
-    rc = run_pipeline(e, e->h_text, e->h_offs, n_utt, total, e->h_slot, e->h_role, ts_us ? e->h_ts : nullptr,
-                      e->h_out, out_cap, e->h_out_offs, e->h_spans, span_cap, e->h_ctx, st);
+    rc = (window ? run_window : run_pipeline)(e, e->h_text, e->h_offs, n_utt, total, e->h_slot, e->h_role,
+                                              ts_us ? e->h_ts : nullptr, e->h_out, out_cap, e->h_out_offs, e->h_spans,
+                                              span_cap, e->h_ctx, st);
     if (rc) return rc;
     uint64_t tot[3];
     rc = pii_sync(e, tot);
@@ -2220,6 +3093,86 @@ int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets
     if (n_spans) *n_spans = (uint32_t)tot[1];
     if (ctx_info && n_utt) HIPCHK(hipMemcpy(ctx_info, e->h_ctx, n_utt * 2, hipMemcpyDeviceToHost));
     return PII_OK;
+}
+
+int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
+                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream) {
+    if (!e || !d_offsets || !d_slot || !d_role || !d_out_offsets) return PII_E_ARG;
+    if (n_utt > 0 && (!d_bytes || !d_out || !d_spans)) return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    uint64_t tb[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(tb, d_offsets, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(tb + 1, d_offsets + n_utt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (tb[1] < tb[0]) return PII_E_ARG;
+    return (window ? run_window : run_pipeline)(e, d_bytes, d_offsets, n_utt, tb[1] - tb[0], d_slot, d_role, d_ts,
+                                                d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx_info, st);
+}
+}  // namespace
+
+extern "C" {
+
+int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                    const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
+                    uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
+                    int16_t* ctx_info) {
+    return host_call(e, false, bytes, offsets, n_utt, conv_slot, role, ts_us, out_bytes, out_cap, out_offsets, spans,
+                     span_cap, n_spans, ctx_info);
+}
+
+int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
+    if (!e || window_n == 0 || window_n > WN_MAX || slot_bytes < 64 || slot_bytes % 16) return PII_E_ARG;
+    if (!e->window_ok) {
+        e->err = "a detector can match '\\n' or a text edge: windows cannot be re-scanned incrementally";
+        return PII_E_RULES;
+    }
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const size_t ns = std::max<uint32_t>(1, e->n_slots);
+    int rc;
+    if ((rc = grow(e, e->wr_desc, ns * window_n)) || (rc = grow(e, e->wr_cnt, ns)) || (rc = grow(e, e->wr_head, ns)) ||
+        (rc = grow(e, e->wr_arena, ns * (size_t)slot_bytes)))
+        return rc;
+    HIPCHK(hipMemset(e->wr_cnt, 0, ns * 4));
+    HIPCHK(hipMemset(e->wr_head, 0, ns * 4));
+    e->win_n = window_n;
+    e->win_slot_bytes = slot_bytes;
+    return PII_OK;
+}
+
+int pii_window_reset(pii_engine* e, uint32_t slot) {
+    if (!e || e->win_n == 0 || slot >= e->n_slots) return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const uint32_t z = 0;
+    HIPCHK(hipMemcpy(e->wr_cnt + slot, &z, 4, hipMemcpyHostToDevice));
+    return PII_OK;
+}
+
+int pii_window_count(pii_engine* e, uint32_t slot, uint32_t* n_entries) {
+    if (!e || e->win_n == 0 || slot >= e->n_slots || !n_entries) return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(n_entries, e->wr_cnt + slot, 4, hipMemcpyDeviceToHost));
+    return PII_OK;
+}
+
+int pii_rescan_window(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                      const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
+                      uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
+                      int16_t* win_ctx) {
+    return host_call(e, true, bytes, offsets, n_utt, conv_slot, role, ts_us, out_bytes, out_cap, out_offsets, spans,
+                     span_cap, n_spans, win_ctx);
+}
+
+int pii_rescan_window_device(pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                             const uint32_t* d_conv_slot, const uint8_t* d_role, const int64_t* d_ts_us,
+                             uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets, pii_span* d_spans,
+                             uint32_t span_cap, int16_t* d_win_ctx, void* stream) {
+    return device_call(e, true, d_bytes, d_offsets, n_utt, d_conv_slot, d_role, d_ts_us, d_out_bytes, out_cap,
+                       d_out_offsets, d_spans, span_cap, d_win_ctx, stream);
 }
 
 int pii_context_get(pii_engine* e, uint32_t slot, int32_t* group, int64_t* ts_us) {

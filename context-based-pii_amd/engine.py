@@ -23,7 +23,8 @@ ERROR_NAMES = {PII_E_ARG: "PII_E_ARG", PII_E_RULES: "PII_E_RULES", PII_E_DEVICE:
 EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_type_name", "pii_context_group_type",
            "pii_last_error", "pii_scan_redact", "pii_scan_redact_device", "pii_sync", "pii_context_get",
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
-           "pii_last_timings_ex", "pii_last_queue_sizes"]
+           "pii_last_timings_ex", "pii_last_queue_sizes", "pii_window_enable", "pii_window_reset",
+           "pii_window_count", "pii_rescan_window", "pii_rescan_window_device"]
 
 
 class PiiError(RuntimeError):
@@ -86,6 +87,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_last_timings.argtypes = [P, c.POINTER(c.c_float)]
     lib.pii_last_timings_ex.argtypes = [P, c.POINTER(c.c_float), c.c_uint32]
     lib.pii_last_queue_sizes.argtypes = [P, U64, U64]
+    lib.pii_window_enable.argtypes = [P, c.c_uint32, c.c_uint32]
+    lib.pii_window_reset.argtypes = [P, c.c_uint32]
+    lib.pii_window_count.argtypes = [P, c.c_uint32, U32]
+    lib.pii_rescan_window.argtypes = lib.pii_scan_redact.argtypes
+    lib.pii_rescan_window_device.argtypes = lib.pii_scan_redact_device.argtypes
     for name in EXPORTS:
         if name != "pii_last_error":
             getattr(lib, name).restype = c.c_int
@@ -133,6 +139,7 @@ class Engine:
         self.lib.pii_engine_info(self.h, ctypes.byref(info))
         self.info = info
         self.n_slots = n_conv_slots
+        self.window_n = 0
         self.type_names = [self._name(t) for t in range(info.n_types)]
         self.group_types = [self.type_names[self.lib.pii_context_group_type(self.h, g)]
                             for g in range(info.n_context_groups)]
@@ -167,30 +174,64 @@ class Engine:
     # ------------------------------------------------------------------ host-buffer batch API
     def scan_redact(self, texts: Sequence[bytes], conv_slot: Sequence[int], role: Sequence[int],
                     ts_us: Optional[Sequence[int]] = None) -> BatchResult:
+        return self._host_call(self.lib.pii_scan_redact, "pii_scan_redact", texts, conv_slot, role, ts_us, 1)
+
+    def rescan_window(self, texts: Sequence[bytes], conv_slot: Sequence[int], role: Sequence[int],
+                      ts_us: Optional[Sequence[int]] = None) -> BatchResult:
+        """Window re-scan (a12): row i's result = its conversation's redacted "\\n".join(last N
+        utterances ending at row i); spans are window offsets; ctx_info = the window's context group."""
+        n = max(1, self.window_n)
+        return self._host_call(self.lib.pii_rescan_window, "pii_rescan_window", texts, conv_slot, role, ts_us, n)
+
+    def window_enable(self, window_n: int = 5, slot_bytes: int = 8192) -> None:
+        rc = self.lib.pii_window_enable(self.h, window_n, slot_bytes)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_window_enable")
+        self.window_n = window_n
+
+    def window_reset(self, slot: int) -> None:
+        rc = self.lib.pii_window_reset(self.h, slot)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_window_reset")
+
+    def window_count(self, slot: int) -> int:
+        n = ctypes.c_uint32()
+        rc = self.lib.pii_window_count(self.h, slot, ctypes.byref(n))
+        if rc != PII_OK:
+            raise self._err(rc, "pii_window_count")
+        return int(n.value)
+
+    def rescan_window_device(self, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,
+                             d_spans, span_cap, d_ctx=None, stream=None) -> None:
+        rc = self.lib.pii_rescan_window_device(self.h, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out,
+                                               out_cap, d_out_offsets, d_spans, span_cap, d_ctx, stream)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_rescan_window_device")
+
+    def _host_call(self, fn, name, texts, conv_slot, role, ts_us, mult) -> BatchResult:
         data, offs = pack(texts)
         n = len(texts)
         slot = np.ascontiguousarray(conv_slot, dtype=np.uint32)
         rl = np.ascontiguousarray(role, dtype=np.uint8)
         ts = None if ts_us is None else np.ascontiguousarray(ts_us, dtype=np.int64)
-        out_cap = int(offs[-1]) + 48 * max(1, n) + 64
-        span_cap = max(16, int(offs[-1]) // 3 + n)
+        out_cap = mult * (int(offs[-1]) + 48 * max(1, n)) + 64
+        span_cap = max(16, mult * (int(offs[-1]) // 3 + n))
         for _ in range(2):
             out = np.empty(out_cap, dtype=np.uint8)
             out_offs = np.zeros(n + 1, dtype=np.uint64)
             spans = np.empty(span_cap, dtype=SPAN_DTYPE)
             ns = ctypes.c_uint32(0)
             ctx = np.empty(n, dtype=np.int16)
-            rc = self.lib.pii_scan_redact(self.h, _ptr(data) if len(data) else None, _ptr(offs), n, _ptr(slot),
-                                          _ptr(rl), _ptr(ts), _ptr(out), out_cap, _ptr(out_offs), _ptr(spans),
-                                          span_cap, ctypes.byref(ns), _ptr(ctx))
+            rc = fn(self.h, _ptr(data) if len(data) else None, _ptr(offs), n, _ptr(slot), _ptr(rl), _ptr(ts),
+                    _ptr(out), out_cap, _ptr(out_offs), _ptr(spans), span_cap, ctypes.byref(ns), _ptr(ctx))
             if rc == PII_E_CAPACITY:
                 out_cap = int(out_offs[-1]) + 64
                 span_cap = int(ns.value) + 16
                 continue
             if rc != PII_OK:
-                raise self._err(rc, "pii_scan_redact")
+                raise self._err(rc, name)
             return BatchResult(out[:int(out_offs[-1])], out_offs, spans[:ns.value].copy(), ctx)
-        raise self._err(PII_E_CAPACITY, "pii_scan_redact")
+        raise self._err(PII_E_CAPACITY, name)
 
     # ------------------------------------------------------------------ device-buffer API (torch)
     def scan_redact_device(self, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,

@@ -130,6 +130,43 @@ int pii_last_timings_ex(struct pii_engine* e, float* ms, uint32_t n);
  * (what the roofline accounting of k_scan counts as written) */
 int pii_last_queue_sizes(struct pii_engine* e, uint64_t* pairs, uint64_t* events);
 
+/* ---------------------------------------------------------------- multi-turn window re-scan (a12)
+ * Replaces the aggregator's sliding-window re-scan (README.md:131-134, 159-168: keep the last N
+ * utterances of a conversation -- N = 5, transcript_aggregator_service/cloudbuild.yaml:33 -- join
+ * them with "\n" and send the joined text through handle_customer_utterance, main.py:386-425) and
+ * the Redis list that held the window.  The window history lives in HBM per conversation slot
+ * (`slot_bytes` each) and keeps, per utterance, its text and its resident detector candidates, so a
+ * re-scan scans only the NEW utterance; the rest of the window costs a hotword re-check where a
+ * proximity window crosses a "\n", the context variant, and the output copy.  Output per row =
+ * redact("\n".join(window ending at that row), current expected_pii_type) bit-exactly (SURVEY A.9,
+ * oracle/pii_oracle.py window_rescan).  Needs rules where no detector can match '\n' or a text edge
+ * (the shipped rules), else PII_E_RULES. */
+#define PII_WINDOW_MAX 8
+/* allocate the per-slot window history (n_conv_slots * slot_bytes of HBM); window_n <= PII_WINDOW_MAX,
+ * slot_bytes a multiple of 16 (a window must fit: its utterances + 16 B per resident candidate) */
+int pii_window_enable(struct pii_engine* e, uint32_t window_n, uint32_t slot_bytes);
+/* forget a conversation's window (the /conversation-ended endpoint, aggregator main.py) */
+int pii_window_reset(struct pii_engine* e, uint32_t slot);
+int pii_window_count(struct pii_engine* e, uint32_t slot, uint32_t* n_entries);
+/* Batch contract as pii_scan_redact (rows of a conversation contiguous, in order).  Each row is
+ * appended to its conversation's window and produces the redacted window text ending at that row:
+ *   out_bytes/out_offsets : one redacted window per row
+ *   spans                 : window findings, utt = row, start/end = byte offsets in the JOINED window
+ *   win_ctx               : optional int16[n_utt], the context group the window used (-1 none): the
+ *                           expected_pii_type a request right after the row would GET (an AGENT row's
+ *                           own keyword hit, else the live record)
+ * AGENT rows update the conversation context exactly as in pii_scan_redact (so passing a row to both
+ * calls is idempotent).  On any error nothing is committed (context, window history). */
+int pii_rescan_window(struct pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                      const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us,
+                      uint8_t* out_bytes, uint64_t out_cap, uint64_t* out_offsets,
+                      pii_span* spans, uint32_t span_cap, uint32_t* n_spans, int16_t* win_ctx);
+int pii_rescan_window_device(struct pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                             uint32_t n_utt, const uint32_t* d_conv_slot, const uint8_t* d_role,
+                             const int64_t* d_ts_us, uint8_t* d_out_bytes, uint64_t out_cap,
+                             uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
+                             int16_t* d_win_ctx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -178,3 +178,100 @@ class TableSim:
             pos = e
         out.append(text[pos:])
         return b"".join(out)
+
+    # ---------------------------------------------------------------- window re-scan (a12)
+    def type_hot_any(self, t: int) -> List[int]:
+        """hotword rules type t has in ANY context variant (k_win_eval's resident bits)"""
+        hs = set()
+        for v in range(self.V):
+            for k in range(int(self.rule_off[v * self.T + t]), int(self.rule_off[v * self.T + t + 1])):
+                hs.add(int(self.rule_ids[k]))
+        return sorted(hs)
+
+    def resident_cands(self, text: bytes):
+        """Variant-independent candidates of one utterance, as k_win_eval + k_win_cands build them:
+        finditer per pattern, validator-passing, inner hotword bits (windows clipped to the text)."""
+        events = self.scan(text, agent=False)
+        cur = [0] * self.P
+        out = []
+        for pos, sd, sk in sorted(events):
+            cd, _ = self._classes(text, pos)
+            a = int(self.dacc[sd, cd])
+            for i in range(int(self.d_off[a]), int(self.d_off[a + 1])):
+                p = int(self.d_ids[i])
+                if pos < cur[p]:
+                    continue
+                e = self.first_run(p, text, pos)
+                if e < 0:
+                    continue
+                cur[p] = e
+                val = int(self.det_val[p])
+                if val and not self.validators[val](text[pos:e]):
+                    continue
+                hot = 0
+                for h in self.type_hot_any(int(self.det_type[p])):
+                    wb, wa = int(self.hot_rule[h][0]), int(self.hot_rule[h][1])
+                    if (wb > 0 and self.hot_run(h, text[max(0, pos - wb):pos])) or \
+                            (wa > 0 and self.hot_run(h, text[e:e + wa])):
+                        hot |= 1 << h
+                out.append((pos, e, p, hot))
+        return out
+
+    def window_select(self, entries, v: int):
+        """k_win_select: entries = [(text, resident cands)] oldest first; findings in window offsets."""
+        W = b"\n".join(t for t, _ in entries)
+        O, o = [], 0
+        for t, _ in entries:
+            O.append(o)
+            o += len(t) + 1
+        minlik = int(self.minlik[v])
+        kept, max_end = [], 0
+        for j, (text, cands) in enumerate(entries):
+            oj, nw = O[j], len(entries)
+            last_ex = {}
+            best, s = None, -1
+
+            def flush():
+                nonlocal max_end
+                if best is not None and oj + s >= max_end:
+                    _, (ss, e, t, lik) = best
+                    kept.append((oj + ss, oj + e, t, lik))
+                    max_end = oj + e
+            for (cs, e, p, hot) in cands:
+                if cs != s:
+                    flush()
+                    best, s = None, cs
+                t = int(self.det_type[p])
+                if not self.enabled[v, t]:
+                    continue
+                lik = int(self.det_lik[p])
+                for k in range(int(self.rule_off[v * self.T + t]), int(self.rule_off[v * self.T + t + 1])):
+                    h = int(self.rule_ids[k])
+                    wb, wa, fixed, rel = [int(x) for x in self.hot_rule[h]]
+                    cb = wb > 0 and s < wb and j > 0
+                    ca = wa > 0 and e + wa > len(text) and j + 1 < nw
+                    if (hot >> h) & 1:
+                        hit = True
+                    elif not cb and not ca:
+                        hit = False
+                    else:
+                        ps, pe = oj + s, oj + e
+                        hit = (wb > 0 and self.hot_run(h, W[max(0, ps - wb):ps])) or \
+                              (wa > 0 and self.hot_run(h, W[pe:pe + wa]))
+                    if hit:
+                        lik = fixed if fixed else min(5, max(1, lik + rel))
+                if lik < minlik:
+                    if t in self.excluder_types:
+                        last_ex[p] = None
+                    continue
+                if t in self.excluder_types:
+                    last_ex[p] = (s, e, t)
+                xs = set(int(x) for x in self.excl_ids[int(self.excl_off[v * self.T + t]):int(self.excl_off[v * self.T + t + 1])])
+                if xs and any(g is not None and q != p and g[2] in xs and g[0] <= s and e <= g[1]
+                              for q, g in last_ex.items()):
+                    continue
+                key = (-(e - s), -lik, t)
+                if best is None or key < best[0]:
+                    best = (key, (s, e, t, lik))
+            flush()
+        return W, kept

@@ -1,0 +1,122 @@
+"""Window re-scan (a12) on the GPU vs the oracle's full re-scan of the joined window.
+
+pii_rescan_window keeps each conversation's last N utterances (text + resident candidates) in HBM
+and scans only the new rows; the bar is bit-exact redacted window bytes, window spans and window
+context against oracle.process_window_rows, which re-redacts "\\n".join(window) from scratch.
+"""
+import random
+
+import pytest
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def weng(compiled):
+    E = pkg("engine")
+    e = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
+    e.window_enable(5, 8192)
+    yield e
+    e.close()
+
+
+def _check(eng, oracle_cfg, calls, n=5, state=None):
+    """calls: list of batches of rows (conv_slot, role, text, ts); each batch keeps a conversation's
+    rows contiguous.  Windows persist across batches (engine ring vs oracle history)."""
+    from oracle import pii_oracle as O
+    store, hist = state if state else (O.ContextStore(), {})
+    groups = list(oracle_cfg.context_keywords.keys())
+    for rows in calls:
+        res = eng.rescan_window([t for _, _, t, _ in rows], [c for c, _, _, _ in rows], [r for _, r, _, _ in rows],
+                                [s for _, _, _, s in rows])
+        exp = O.process_window_rows(rows, oracle_cfg, n=n, store=store, history=hist)
+        for i, ((red, fs, et), row) in enumerate(zip(exp, rows)):
+            assert res.text(i) == red, (i, row, res.text(i), red)
+            m = res.spans["utt"] == i
+            got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"])) for s in res.spans[m]]
+            assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], (i, row)
+            g = int(res.ctx_info[i])
+            assert (groups[g] if g >= 0 else None) == et, (i, row)
+    return store, hist
+
+
+def _stream(corp, slot_base):
+    rows = []
+    for i in range(corp.n):
+        a, b = int(corp.offsets[i]), int(corp.offsets[i + 1])
+        rows.append((slot_base + int(corp.conv_slot[i]), int(corp.role[i]), corp.data[a:b].tobytes(),
+                     int(corp.ts_us[i])))
+    return rows
+
+
+def test_window_streamed_one_row_per_conversation(weng, oracle_cfg):
+    """config 3 shape: every call carries the next utterance of every conversation"""
+    synth = pkg("synth")
+    bank = synth.build_bank(400, 900, seed=21)
+    corp = synth.make_corpus(60, 14, bank, seed=22)
+    per_conv = {}
+    for r in _stream(corp, 0):
+        per_conv.setdefault(r[0], []).append(r)
+    state = None
+    for k in range(14):
+        state = _check(weng, oracle_cfg, [[per_conv[c][k] for c in sorted(per_conv)]], state=state)
+
+
+def test_window_runs_within_a_batch(weng, oracle_cfg):
+    """several rows of one conversation in one call: the window mixes resident and batch rows"""
+    synth = pkg("synth")
+    bank = synth.build_bank(400, 900, seed=31)
+    corp = synth.make_corpus(40, 23, bank, seed=32)
+    per_conv = {}
+    for r in _stream(corp, 100):
+        per_conv.setdefault(r[0], []).append(r)
+    rng = random.Random(5)
+    state = None
+    done = {c: 0 for c in per_conv}
+    while any(done[c] < len(per_conv[c]) for c in per_conv):
+        batch = []
+        for c in sorted(per_conv):
+            k = rng.choice([0, 1, 2, 3, 7])
+            batch += per_conv[c][done[c]:done[c] + k]
+            done[c] = min(len(per_conv[c]), done[c] + k)
+        if batch:
+            state = _check(weng, oracle_cfg, [batch], state=state)
+
+
+def test_window_halo_and_edges(weng, oracle_cfg):
+    from oracle import pii_oracle as O
+    A, C = O.ROLE_AGENT, O.ROLE_CUSTOMER
+    rows = [(900, C, b"please read me your social security", 1), (900, C, b"987654321 thanks", 2),
+            (901, A, b"what is your driver's license", 1), (901, C, b"", 2), (901, C, b"G223456789", 3),
+            (901, C, b"and passport E98765432", 4), (901, C, b"x" * 700 + b" 4141-1212-2323-5009", 5),
+            (902, C, b"card number\n", 1), (902, C, b"\n", 2), (902, C, "é 4141 1212 2323 5009".encode(), 3),
+            (903, A, b"email?", 1), (903, C, b"jane.doe@example.com @TechieTom", 2)]
+    state = _check(weng, oracle_cfg, [rows])
+    state = _check(weng, oracle_cfg, [[]], state=state)              # empty batch
+    assert weng.window_count(901) == 5
+    weng.window_reset(901)                                           # /conversation-ended
+    state[1].pop(901)
+    assert weng.window_count(901) == 0
+    _check(weng, oracle_cfg, [[(901, C, b"SSN 123-45-6788", 9), (901, C, b"ok", 10)]], state=state)
+
+
+def test_window_history_overflow_is_atomic(compiled, oracle_cfg):
+    """a window that does not fit its slot fails the call and commits nothing"""
+    from oracle import pii_oracle as O
+    E = pkg("engine")
+    eng = E.Engine(compiled.blob, device=0, n_conv_slots=8)
+    try:
+        eng.window_enable(5, 256)
+        C = O.ROLE_CUSTOMER
+        eng.rescan_window([b"a" * 100], [1], [C], [1])
+        assert eng.window_count(1) == 1
+        with pytest.raises(E.PiiError) as ei:
+            eng.rescan_window([b"b" * 200], [1], [C], [2])
+        assert ei.value.code == E.PII_E_NOMEM
+        assert eng.window_count(1) == 1
+        res = eng.rescan_window([b"c" * 10], [1], [C], [3])
+        assert res.text(0) == b"a" * 100 + b"\n" + b"c" * 10
+    finally:
+        eng.close()
