@@ -131,7 +131,12 @@ def main():
     ap.add_argument("--utt-per-conv", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["scan", "window"], default="scan",
+                    help="scan = config 2 (headline); window = config 3 multi-turn re-scan")
+    ap.add_argument("--window-n", type=int, default=5)
     args = ap.parse_args()
+    if args.workload == "window":
+        return window_main(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,6 +259,146 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- config 3: window re-scan
+def _cpu_window_work(rng):
+    from oracle import pii_oracle as O
+    cfg = O.RuleConfig.load()
+    d, o, r, c, t = _CPU["data"], _CPU["offs"], _CPU["role"], _CPU["conv"], _CPU["ts"]
+    lo, hi = rng
+    rows = [(int(c[i]), int(r[i]), d[int(o[i]):int(o[i + 1])].tobytes(), int(t[i])) for i in range(lo, hi)]
+    n = _CPU["win_n"]
+    t0 = time.perf_counter()
+    O.process_window_rows(rows, cfg, n=n)
+    return time.perf_counter() - t0, int(o[hi] - o[lo])
+
+
+def cpu_window_baseline(bank, n_win: int, seconds: float = 15.0):
+    """oracle.process_window_rows (full re-scan of every joined window: what the reference does per
+    utterance) over whole conversations, multi-process on the host; MB/s of NEW utterance bytes."""
+    cores = min(16, os.cpu_count() or 1)
+    probe = synth.corpus_meta(4, 100, bank, seed=synth.SEED + 7)
+    pdata = synth.gather_bytes(probe, bank)
+    _cpu_init(pdata, probe.offsets.astype(np.int64), probe.role, probe.conv_slot, probe.ts_us)
+    _CPU["win_n"] = n_win
+    dt, nb = _cpu_window_work((0, probe.n))
+    conv_rate = 4 / max(dt, 1e-6)
+    n_conv = int(min(20000, max(cores * 4, conv_rate * cores * seconds * 0.5)))
+    meta = synth.corpus_meta(n_conv, 100, bank, seed=synth.SEED + 7)
+    data = synth.gather_bytes(meta, bank)
+    chunks = [(i * 100, (i + 1) * 100) for i in range(n_conv)]
+    _cpu_init(data, meta.offsets.astype(np.int64), meta.role, meta.conv_slot, meta.ts_us)
+    _CPU["win_n"] = n_win
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_window_work, chunks, chunksize=max(1, len(chunks) // (cores * 8)))
+    wall = time.perf_counter() - t0
+    nbytes = sum(b for _, b in res)
+    return {"value": round(nbytes / wall / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
+            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e6:.1f} MB new bytes), every utterance "
+                      f"followed by a full oracle re-scan of its window of {n_win} (process_window_rows), "
+                      f"multiprocessing fork pool of {cores}, wall {wall:.1f}s"}
+
+
+def window_main(args):
+    """BASELINE config 3: multi-turn sliding-window re-scan, N = --window-n, over --conversations
+    concurrent conversations on one GPU.  A step = one pii_rescan_window_device call carrying the next
+    utterance of every conversation (the aggregator's stream); each row yields its redacted window."""
+    import torch
+    eng_mod = importlib.import_module("context-based-pii_amd.engine")
+    C, U, N = args.conversations, args.utt_per_conv, args.window_n
+    bank = synth.build_bank(16384, 16384, seed=synth.SEED)
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_window_baseline(bank, N, args.cpu_seconds)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    meta = synth.step_major(synth.corpus_meta(C, U, bank, seed=synth.SEED), bank, C, U)
+    text, offs = gpu_corpus(meta, bank, dev)
+    slot = torch.from_numpy(meta.conv_slot.view(np.int32)).to(dev)
+    role = torch.from_numpy(meta.role).to(dev)
+    ts = torch.from_numpy(meta.ts_us).to(dev)
+    step_bytes = [int(meta.offsets[(k + 1) * C] - meta.offsets[k * C]) for k in range(U)]
+    out_cap = (N + 1) * max(step_bytes) + 64 * N * C
+    span_cap = 8 * N * C
+    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    d_oo = torch.empty(C + 1, dtype=torch.int64, device=dev)
+    d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
+    d_ctx = torch.empty(C, dtype=torch.int16, device=dev)
+    comp = compiler.compile_default()
+    eng = eng_mod.Engine(comp.blob, device=0, n_conv_slots=C)
+    eng.window_enable(N, 8192)
+    torch.cuda.synchronize()
+
+    def step(k):
+        o = offs.data_ptr() + 8 * k * C
+        eng.rescan_window_device(text.data_ptr(), o, C, slot.data_ptr() + 4 * k * C, role.data_ptr() + k * C,
+                                 ts.data_ptr() + 8 * k * C, d_out.data_ptr(), out_cap, d_oo.data_ptr(),
+                                 d_sp.data_ptr(), span_cap, d_ctx.data_ptr())
+        ob, ns, fl = eng.sync()
+        if fl:
+            raise RuntimeError(f"engine error flags {fl}")
+        return ob, ns
+
+    warm = max(args.warmup, N)                 # windows are full from step N-1 on
+    if warm + args.steps > U:
+        raise SystemExit(f"--warmup + --steps must be <= --utt-per-conv ({U})")
+    for k in range(warm):
+        step(k)
+    torch.cuda.synchronize()
+    per_stage = np.zeros(6)
+    k_red = 0.0
+    new_b = out_b = spans = 0
+    t0 = time.perf_counter()
+    for k in range(warm, warm + args.steps):
+        ob, ns = step(k)
+        per_stage += np.array(eng.timings())
+        k_red += eng.kernel_timings()["k_redact"]
+        new_b += step_bytes[k]
+        out_b += ob
+        spans += ns
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    K = args.steps
+    per_stage /= K
+    k_red /= K
+    # window bytes read to write the outputs: every window's utterances and separators
+    lens = (meta.offsets[1:] - meta.offsets[:-1]).astype(np.int64).reshape(U, C)
+    win_in = 0
+    for k in range(warm, warm + K):
+        lo = max(0, k - N + 1)
+        win_in += int(lens[lo:k + 1].sum()) + (k - lo) * C
+    t_pipe = per_stage[5] / 1e3 * K
+    # algorithmic bytes (SURVEY 8(d) config 3): new bytes + window bytes re-read for the output copy +
+    # window output written + ring commit of the new bytes + offsets/state (8+8+4+1+8 B per row)
+    B = new_b + win_in + out_b + new_b + K * C * (8 + 8 + 4 + 1 + 8) + 16 * spans
+    red_B = win_in + out_b + K * C * 24 + 32 * spans
+    line = {
+        "metric": "multi-turn window re-scan: new transcript MB/s (each utterance -> its redacted window of N)",
+        "value": round(new_b / elapsed / 1e6, 1), "unit": "MB/s", "n_gpus": 1, "steps": K, "warmup": warm,
+        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"config3: {C} concurrent conversations, window N={N}, one new utterance per "
+                               f"conversation per step (pii_rescan_window_device), expected_pii_type context",
+                   "rows_per_step": C, "parallelism": "conversation-sharded x1"},
+        "windows_per_s": round(K * C / elapsed, 1),
+        "window_output_MBps": round(out_b / elapsed / 1e6, 1),
+        "naive_equivalent_bytes_rescanned_per_step": int(win_in / K),
+        "new_bytes_per_step": int(new_b / K),
+        "stages_ms": {k: round(float(v), 4) for k, v in zip(
+            ["scan+pairs", "context", "first+cands", "select+offsets", "redact+commit", "pipeline"], per_stage)},
+        "pipeline": {"algorithmic_bytes": int(B / K), "GBps": round(B / t_pipe / 1e9, 1),
+                     "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
+        "roofline": {"bound": "hbm", "kernel": "k_win_redact", "achieved": round(red_B / K / (k_red / 1e3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(red_B / K / (k_red / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "algorithmic_bytes": int(red_B / K), "launch_ms": round(k_red, 4)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

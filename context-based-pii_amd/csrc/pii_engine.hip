@@ -41,7 +41,8 @@ constexpr int SCAN_BLOCK = 512;
 constexpr int CTX_BLOCK = 1024;
 constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
-constexpr uint32_t BYTES_PER_LANE = 1024;
+constexpr uint32_t BYTES_PER_LANE = 1024;    // largest scan lane (big batches)
+constexpr uint32_t MIN_LANE_SHIFT = 7;        // smallest scan lane, 128 B (small batches need lanes, not bytes)
 constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
@@ -88,7 +89,7 @@ struct RulesDev {
 // also writes every row's defaults (no findings: out_len = len, n_find = 0; keyword group = the
 // always-present group for AGENT rows, else -1) with coalesced stores.
 __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role, uint32_t n_utt,
-                              uint32_t n_chunks, int kw_always, uint32_t* __restrict__ first_utt,
+                              uint32_t n_chunks, uint32_t lane_shift, int kw_always, uint32_t* __restrict__ first_utt,
                               uint32_t* __restrict__ out_len, uint32_t* __restrict__ n_find,
                               int16_t* __restrict__ kw, uint32_t* __restrict__ wc_n) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -96,8 +97,8 @@ __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* 
     const uint64_t base = offs[0];
     const uint64_t su = offs[u] - base;
     uint64_t c_lo = 0;
-    if (u > 0) c_lo = (offs[u - 1] - base) / BYTES_PER_LANE + 1;
-    uint64_t c_hi = (u == n_utt) ? n_chunks : su / BYTES_PER_LANE;
+    if (u > 0) c_lo = ((offs[u - 1] - base) >> lane_shift) + 1;
+    uint64_t c_hi = (u == n_utt) ? n_chunks : su >> lane_shift;
     if (c_hi > n_chunks) c_hi = n_chunks;
     for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
     if (u < n_utt) {
@@ -1475,64 +1476,80 @@ struct WEntry {
     uint32_t len, nc;
 };
 
-// The window of row u, oldest first: the newest ring entries of u's conversation, then u's
-// same-conversation predecessors in the batch, then u.  Returns the entry count (>= 1).
-__device__ __forceinline__ int win_entries(const WinRing& W, const WinBatch& B, uint32_t u, WEntry* E) {
-    const uint32_t sl = B.slot[u];
+// The window of row u, oldest first: the r newest ring entries of u's conversation, then u's m
+// same-conversation predecessors in the batch, then u.  Entries are produced on demand (win_at), so
+// the kernels keep no per-thread entry arrays (which would live in scratch memory).
+struct WinIt {
+    uint32_t u, sl, m, r, head;
+    int nw;
+};
+
+__device__ __forceinline__ WinIt win_begin(const WinRing& W, const WinBatch& B, uint32_t u) {
+    WinIt it;
+    it.u = u;
+    it.sl = B.slot[u];
     uint32_t m = 0;
-    while (m + 1 < W.N && u >= m + 1 && B.slot[u - m - 1] == sl) ++m;
-    uint32_t r = 0;
-    if (m + 1 < W.N && sl < W.n_slots) r = min(W.N - 1 - m, W.cnt[sl]);
-    int nw = 0;
-    if (r) {
-        const uint32_t head = W.head[sl];
-        const uint8_t* ar = W.arena + (size_t)sl * W.slot_bytes;
-        for (uint32_t i = 0; i < r; ++i) {
-            const WDesc D = W.desc[(size_t)sl * W.N + (head + W.N - r + i) % W.N];
-            E[nw].t = ar + D.off + 16u * D.nc;
-            E[nw].c = reinterpret_cast<const WCand*>(ar + D.off);
-            E[nw].len = D.len;
-            E[nw].nc = D.nc;
-            ++nw;
-        }
+    while (m + 1 < W.N && u >= m + 1 && B.slot[u - m - 1] == it.sl) ++m;
+    uint32_t r = 0, head = 0;
+    if (m + 1 < W.N && it.sl < W.n_slots) {
+        r = min(W.N - 1 - m, W.cnt[it.sl]);
+        head = W.head[it.sl];
     }
-    for (uint32_t i = 0; i <= m; ++i) {
-        const uint32_t v = u - m + i;
-        const uint64_t a = B.offs[v];
-        E[nw].t = B.text + a;
-        E[nw].nc = B.wc_n[v];
-        E[nw].c = B.wc + (E[nw].nc ? B.wc_first[v] : 0u);
-        E[nw].len = (uint32_t)(B.offs[v + 1] - a);
-        ++nw;
-    }
-    return nw;
+    it.m = m;
+    it.r = r;
+    it.head = head;
+    it.nw = (int)(r + m + 1);
+    return it;
 }
 
-// Unanchored HOT DFA over window positions [lo, hi) (entry j starts at window offset O[j]; entries
-// are joined by '\n'), window edges as text edges: the proximity test of a candidate whose window
-// reaches into a neighbour utterance.
-__device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WEntry* E, const uint32_t* O, int nw,
-                            uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ WEntry win_at(const WinRing& W, const WinBatch& B, const WinIt& it, int j) {
+    WEntry E;
+    if ((uint32_t)j < it.r) {
+        const WDesc D = W.desc[(size_t)it.sl * W.N + (it.head + W.N - it.r + (uint32_t)j) % W.N];
+        const uint8_t* a = W.arena + (size_t)it.sl * W.slot_bytes + D.off;
+        E.t = a + 16u * D.nc;
+        E.c = reinterpret_cast<const WCand*>(a);
+        E.len = D.len;
+        E.nc = D.nc;
+    } else {
+        const uint32_t v = it.u - it.m + ((uint32_t)j - it.r);
+        const uint64_t a = B.offs[v];
+        E.t = B.text + a;
+        E.nc = B.wc_n[v];
+        E.c = B.wc + (E.nc ? B.wc_first[v] : 0u);
+        E.len = (uint32_t)(B.offs[v + 1] - a);
+    }
+    return E;
+}
+
+// Unanchored HOT DFA over window positions [lo, hi) (entries joined by '\n'), window edges as text
+// edges: the proximity test of a candidate whose window reaches into a neighbour utterance.
+__device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WinRing& W, const WinBatch& B,
+                            const WinIt& it, uint32_t lo, uint32_t hi) {
     const uint16_t* tr = pool.trans + d[0];
     const uint8_t* cm = pool.cmap + d[2];
     const uint32_t nc = (uint32_t)d[3];
     uint32_t st = (uint32_t)d[4];
-    for (int j = 0; j < nw; ++j) {
-        const uint32_t sl = O[j], sh = O[j] + E[j].len;
-        if (sh < lo) continue;
-        if (sl >= hi) break;
-        const int a = (int)(max(lo, sl) - sl), b = (int)(min(hi, sh) - sl);
-        const uint8_t* t = E[j].t;
-        PII_FOR_BYTES(t, a, b, {
-            const uint32_t x = tr[st * nc + cm[c]];
-            if (x & 0x4000u) return true;
-            st = x & DFA_STATE_MASK;
-        })
-        if (j + 1 < nw && sh >= lo && sh < hi) {
-            const uint32_t x = tr[st * nc + cm['\n']];
-            if (x & 0x4000u) return true;
-            st = x & DFA_STATE_MASK;
+    uint32_t sl = 0;
+    for (int j = 0; j < it.nw; ++j) {
+        const WEntry Ej = win_at(W, B, it, j);
+        const uint32_t sh = sl + Ej.len;
+        if (sh >= lo) {
+            if (sl >= hi) break;
+            const int a = (int)(max(lo, sl) - sl), b = (int)(min(hi, sh) - sl);
+            const uint8_t* t = Ej.t;
+            PII_FOR_BYTES(t, a, b, {
+                const uint32_t x = tr[st * nc + cm[c]];
+                if (x & 0x4000u) return true;
+                st = x & DFA_STATE_MASK;
+            })
+            if (j + 1 < it.nw && sh < hi) {
+                const uint32_t x = tr[st * nc + cm['\n']];
+                if (x & 0x4000u) return true;
+                st = x & DFA_STATE_MASK;
+            }
         }
+        sl = sh + 1;
     }
     return (tr[st * nc + nc - 1] & 0x4000u) != 0;
 }
@@ -1713,10 +1730,9 @@ __global__ __launch_bounds__(256) void k_win_plan(const WinRing W, const WinBatc
         bound[u] = 0;
         return;
     }
-    WEntry E[WN_MAX];
-    const int nw = win_entries(W, B, u, E);
+    const WinIt it = win_begin(W, B, u);
     uint32_t b = 0;
-    for (int j = 0; j < nw; ++j) b += E[j].nc;
+    for (int j = 0; j < it.nw; ++j) b += win_at(W, B, it, j).nc;
     bound[u] = b;
 }
 
@@ -1751,15 +1767,11 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
         if (u == 0) atomicOr(err, (uint32_t)ERR_QUEUE);
         return;
     }
-    WEntry E[WN_MAX];
-    uint32_t O[WN_MAX];
-    const int nw = win_entries(W, B, u, E);
-    uint32_t o = 0;
-    for (int j = 0; j < nw; ++j) {
-        O[j] = o;
-        o += E[j].len + 1;
-    }
-    const uint32_t WL = o - 1;
+    const WinIt it = win_begin(W, B, u);
+    const int nw = it.nw;
+    uint32_t WL = 0;
+    for (int j = 0; j < nw; ++j) WL += win_at(W, B, it, j).len + 1;
+    WL -= 1;
     const int T = R.T;
     const int g = win_ctx[u];
     const int v = g >= 0 ? g + 1 : 0;
@@ -1768,9 +1780,9 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
     uint32_t nf = 0;
     int delta = 0;
     uint32_t max_end = 0;
+    uint32_t oj = 0;
     for (int j = 0; j < nw; ++j) {
-        const WEntry Ej = E[j];
-        const uint32_t oj = O[j];
+        const WEntry Ej = win_at(W, B, it, j);
         int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
         uint32_t ex_valid = 0;
         int s = -1, best_e = -1, best_t = 0, best_lik = 0;
@@ -1813,8 +1825,8 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
                     hit = false;
                 } else {
                     const uint32_t ps = oj + (uint32_t)s, pe = oj + (uint32_t)e;
-                    hit = wb > 0 && hot_run_win(pool, hdesc + 8 * h, E, O, nw, ps > (uint32_t)wb ? ps - wb : 0u, ps);
-                    if (!hit && wa > 0) hit = hot_run_win(pool, hdesc + 8 * h, E, O, nw, pe, min(WL, pe + (uint32_t)wa));
+                    hit = wb > 0 && hot_run_win(pool, hdesc + 8 * h, W, B, it, ps > (uint32_t)wb ? ps - wb : 0u, ps);
+                    if (!hit && wa > 0) hit = hot_run_win(pool, hdesc + 8 * h, W, B, it, pe, min(WL, pe + (uint32_t)wa));
                 }
                 if (hit) {
                     const int fixed = hrule[4 * h + 2], rel = hrule[4 * h + 3];
@@ -1860,6 +1872,7 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
             }
         }
         flush_start();
+        oj += Ej.len + 1;
     }
     n_wfind[u] = nf;
     wout_len[u] = (uint32_t)((int)WL + delta);
@@ -1917,15 +1930,16 @@ __global__ __launch_bounds__(256) void k_win_alloc(const WinRing W, const WinBat
 }
 
 // window output byte `rel` (slow path for windows whose pieces overflow the tile's LDS table)
-__device__ uint8_t win_byte_slow(const RulesDev& R, const WEntry* E, const uint32_t* O, int nw,
+__device__ uint8_t win_byte_slow(const RulesDev& R, const WinRing& W, const WinBatch& B, const WinIt& it,
                                  const pii_span* F, uint32_t nf, uint32_t rel) {
-    uint32_t pout = 0, fi = 0;
-    for (int j = 0; j < nw; ++j) {
-        const uint32_t sh = O[j] + E[j].len;
-        uint32_t pin = O[j];
+    uint32_t pout = 0, fi = 0, oj = 0;
+    for (int j = 0; j < it.nw; ++j) {
+        const WEntry Ej = win_at(W, B, it, j);
+        const uint32_t sh = oj + Ej.len;
+        uint32_t pin = oj;
         while (fi < nf && F[fi].start < sh) {
             const uint32_t run = F[fi].start - pin;
-            if (rel < pout + run) return E[j].t[pin - O[j] + (rel - pout)];
+            if (rel < pout + run) return Ej.t[pin - oj + (rel - pout)];
             pout += run;
             const uint32_t t0 = R.tok_off[F[fi].info_type], tl = R.tok_off[F[fi].info_type + 1] - t0;
             if (rel < pout + tl) return R.tok_bytes[t0 + (rel - pout)];
@@ -1934,10 +1948,11 @@ __device__ uint8_t win_byte_slow(const RulesDev& R, const WEntry* E, const uint3
             ++fi;
         }
         const uint32_t run = sh - pin;
-        if (rel < pout + run) return E[j].t[pin - O[j] + (rel - pout)];
+        if (rel < pout + run) return Ej.t[pin - oj + (rel - pout)];
         pout += run;
         if (rel == pout) return '\n';
         ++pout;
+        oj = sh + 1;
     }
     return 0;
 }
@@ -1965,20 +1980,14 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, c
     const int64_t out_lo = (int64_t)out_offs[u0], out_hi = (int64_t)out_offs[u1];
     const bool mine = (uint32_t)tid < nu;        // WIN_TILE == 64: wavefront 0 owns the windows
     const uint32_t u = u0 + tid;
-    WEntry E[WN_MAX];
-    uint32_t O[WN_MAX];
-    int nw = 0;
+    WinIt it;
+    it.nw = 0;
     uint32_t nf = 0;
     if (mine) {
-        nw = win_entries(W, B, u, E);
-        uint32_t o = 0;
-        for (int j = 0; j < nw; ++j) {
-            O[j] = o;
-            o += E[j].len + 1;
-        }
+        it = win_begin(W, B, u);
         nf = n_wfind[u];
     }
-    const uint32_t cnt = mine ? 2 * nf + 2 * (uint32_t)nw - 1 : 0;
+    const uint32_t cnt = mine ? 2 * nf + 2 * (uint32_t)it.nw - 1 : 0;
     uint32_t incl = cnt;
     if (wid == 0) {
         for (int d = 1; d < 64; d <<= 1) {
@@ -1997,11 +2006,12 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, c
         if (staged) {
             uint32_t pb = incl - cnt;
             uint32_t po = (uint32_t)((int64_t)out_offs[u] - out_lo);
-            uint32_t fi = 0;
-            for (int j = 0; j < nw; ++j) {
-                const uint32_t sh = O[j] + E[j].len;
-                const uint64_t src = (uint64_t)(uintptr_t)E[j].t - O[j];     // window position -> address
-                uint32_t pin = O[j];
+            uint32_t fi = 0, oj = 0;
+            for (int j = 0; j < it.nw; ++j) {
+                const WEntry Ej = win_at(W, B, it, j);
+                const uint32_t sh = oj + Ej.len;
+                const uint64_t src = (uint64_t)(uintptr_t)Ej.t - oj;     // window position -> address
+                uint32_t pin = oj;
                 while (fi < nf && F[fi].start < sh) {
                     const pii_span Fi = F[fi];
                     s_pout[pb] = po;
@@ -2020,12 +2030,13 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, c
                 s_psrc[pb] = src + pin;
                 ++pb;
                 po += sh - pin;
-                if (j + 1 < nw) {
+                if (j + 1 < it.nw) {
                     s_pout[pb] = po;
                     s_psrc[pb] = (uint64_t)(uintptr_t)(R.tok_bytes + R.nl_off);
                     ++pb;
                     po += 1;
                 }
+                oj = sh + 1;
             }
         }
     }
@@ -2034,24 +2045,15 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, c
     if (staged) {
         tile_assemble(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
     } else {
-        // one window at a time per wavefront, byte-granular (wavefront 0 holds the entry lists)
-        if (wid == 0) {
-            for (uint32_t i = 0; i < nu; ++i) {
-                const uint32_t uu = u0 + i;
-                WEntry Ei[WN_MAX];
-                uint32_t Oi[WN_MAX];
-                const int nwi = win_entries(W, B, uu, Ei);
-                uint32_t o = 0;
-                for (int j = 0; j < nwi; ++j) {
-                    Oi[j] = o;
-                    o += Ei[j].len + 1;
-                }
-                const pii_span* F = wfd + fbase[uu];
-                const uint32_t nfi = n_wfind[uu];
-                uint8_t* dst = out + out_offs[uu];
-                const uint32_t olen = (uint32_t)(out_offs[uu + 1] - out_offs[uu]);
-                for (uint32_t rel = lane; rel < olen; rel += 64) dst[rel] = win_byte_slow(R, Ei, Oi, nwi, F, nfi, rel);
-            }
+        // one wavefront per window, byte-granular
+        for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
+            const uint32_t uu = u0 + i;
+            const WinIt iu = win_begin(W, B, uu);
+            const pii_span* F = wfd + fbase[uu];
+            const uint32_t nfi = n_wfind[uu];
+            uint8_t* dst = out + out_offs[uu];
+            const uint32_t olen = (uint32_t)(out_offs[uu + 1] - out_offs[uu]);
+            for (uint32_t rel = lane; rel < olen; rel += 64) dst[rel] = win_byte_slow(R, W, B, iu, F, nfi, rel);
         }
     }
 }
@@ -2205,7 +2207,8 @@ struct pii_engine {
     unsigned long long* hist = nullptr;
     uint32_t* hist_part = nullptr;     // per redact tile, per info type
     // scratch
-    uint64_t cap_bytes = 0;
+    uint64_t cap_bytes = 0, cap_lanes = 0;
+    uint32_t lane_shift = 10, last_lanes = 0;     // scan lane = utterances starting in 2^lane_shift bytes
     uint32_t cap_utt = 0;
     size_t cap_bsum = 0;
     Event* ev = nullptr;
@@ -2318,20 +2321,24 @@ int grow_pairs(pii_engine* e, uint64_t cap) {
     return PII_OK;
 }
 
-int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
+int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lanes) {
     int rc = PII_OK;
 
     if (bytes > e->cap_bytes) {
         const uint64_t nb = std::max<uint64_t>(bytes + bytes / 8, 1 << 16);
         if ((rc = grow(e, e->ev, nb + 1))) return rc;
         if ((rc = grow(e, e->fd, nb / e->R.min_len + 2))) return rc;
-        if ((rc = grow(e, e->first_utt, nb / BYTES_PER_LANE + 2))) return rc;
-        if ((rc = grow(e, e->lane_cnt, nb / BYTES_PER_LANE + 2))) return rc;
-        if ((rc = grow(e, e->lane_ev, nb / BYTES_PER_LANE + 2))) return rc;
-        if ((rc = grow(e, e->bnd, (nb / BYTES_PER_LANE + 2) * LANE_WORDS))) return rc;
-        if ((rc = grow(e, e->lane_pair, nb / BYTES_PER_LANE + 2))) return rc;
-        if ((rc = grow(e, e->lane_np, nb / BYTES_PER_LANE + 2))) return rc;
         e->cap_bytes = nb;
+    }
+    if (n_lanes + 2 > e->cap_lanes) {
+        const uint64_t nl = std::max<uint64_t>(n_lanes + n_lanes / 8 + 2, 1024);
+        if ((rc = grow(e, e->first_utt, nl))) return rc;
+        if ((rc = grow(e, e->lane_cnt, nl))) return rc;
+        if ((rc = grow(e, e->lane_ev, nl))) return rc;
+        if ((rc = grow(e, e->bnd, nl * LANE_WORDS))) return rc;
+        if ((rc = grow(e, e->lane_pair, nl))) return rc;
+        if ((rc = grow(e, e->lane_np, nl))) return rc;
+        e->cap_lanes = nl;
         e->cap_bsum = 0;
     }
     if (n_utt > e->cap_utt) {
@@ -2353,7 +2360,7 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes) {
         e->cap_bsum = 0;
     }
     if (e->cap_bsum == 0) {   // scan block sums: the utterance scans and the per-lane pair-count scan
-        const size_t n = std::max<size_t>(e->cap_utt, e->cap_bytes / BYTES_PER_LANE + 2);
+        const size_t n = std::max<size_t>(e->cap_utt, e->cap_lanes);
         if ((rc = grow(e, e->bsum, n / SCAN_TILE + 2))) return rc;
         e->cap_bsum = n;
     }
@@ -2371,6 +2378,14 @@ int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out,
     k_scan_apply<<<nb, 256, 0, st>>>(in, n, e->bsum, out);
     HIPCHK(hipGetLastError());
     return PII_OK;
+}
+
+// scan lane size for a batch: 1 KiB lanes for big batches, down to 128 B so that a small batch (one
+// re-scan step) still has ~64k lanes to spread over 256 CUs
+uint32_t pick_lane_shift(const pii_engine* e, uint64_t total_bytes) {
+    uint32_t sh = (uint32_t)__builtin_ctz(BYTES_PER_LANE);
+    while (sh > MIN_LANE_SHIFT && (total_bytes >> sh) < (uint64_t)e->n_cu * 256) --sh;
+    return sh;
 }
 
 // queues sized for a batch of `total_bytes`
@@ -2400,7 +2415,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
     HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
-        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, R.kw_always_min,
+        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, R.kw_always_min,
                                                                 e->first_utt, e->out_len, e->n_find, e->kw,
                                                                 win_ctx ? e->wc_n : nullptr);
         if (n_chunks > 0) {
@@ -2451,7 +2466,10 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
         return PII_E_ARG;
     }
-    int rc = ensure_scratch(e, n_utt, total_bytes);
+    e->lane_shift = pick_lane_shift(e, total_bytes);
+    const uint32_t n_chunks = (uint32_t)((total_bytes + (1u << e->lane_shift) - 1) >> e->lane_shift);
+    e->last_lanes = n_chunks;
+    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
     if (rc || (rc = ensure_queues(e, total_bytes))) return rc;
     e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
                                ctx_info, st};
@@ -2459,7 +2477,6 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     const RulesDev& R = e->R;
     int16_t* ctx = ctx_info ? ctx_info : e->ctx;
     e->kev_valid = n_utt > 0 && total_bytes > 0;
-    const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
     // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
     const unsigned long long* pcount =
         n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
@@ -2535,7 +2552,10 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
         return PII_E_ARG;
     }
-    int rc = ensure_scratch(e, n_utt, total_bytes);
+    e->lane_shift = pick_lane_shift(e, total_bytes);
+    const uint32_t n_chunks = (uint32_t)((total_bytes + (1u << e->lane_shift) - 1) >> e->lane_shift);
+    e->last_lanes = n_chunks;
+    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
     if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_window_scratch(e, n_utt))) return rc;
     e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
                                win_ctx, st};
@@ -2543,7 +2563,6 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     const RulesDev& R = e->R;
     int16_t* wctx = win_ctx ? win_ctx : e->wctx;
     e->kev_valid = n_utt > 0 && total_bytes > 0;
-    const uint32_t n_chunks = (uint32_t)((total_bytes + BYTES_PER_LANE - 1) / BYTES_PER_LANE);
     const unsigned long long* pcount =
         n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
     if ((rc = launch_front(e, text, offs, n_utt, n_chunks, slot, role, ts, e->ctx, wctx, pcount, st))) return rc;
@@ -3016,6 +3035,14 @@ int pii_last_queue_sizes(pii_engine* e, uint64_t* pairs, uint64_t* events) {
     if (pairs) *pairs = e->h_totals[3];
     if (events) *events = e->h_totals[4];
     return PII_OK;
+}
+
+int pii_last_stats(pii_engine* e, uint64_t* out, uint32_t n) {
+    if (!e || (!out && n)) return PII_E_ARG;
+    const uint64_t all[6] = {e->h_totals[3], e->h_totals[4], e->last_lanes, 1ull << e->lane_shift, e->h_totals[5],
+                             e->h_totals[1]};
+    for (uint32_t i = 0; i < n && i < 6; ++i) out[i] = all[i];
+    return (int)std::min<uint32_t>(n, 6);
 }
 
 int pii_last_timings_ex(pii_engine* e, float* ms, uint32_t n) {

@@ -23,7 +23,7 @@ ERROR_NAMES = {PII_E_ARG: "PII_E_ARG", PII_E_RULES: "PII_E_RULES", PII_E_DEVICE:
 EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_type_name", "pii_context_group_type",
            "pii_last_error", "pii_scan_redact", "pii_scan_redact_device", "pii_sync", "pii_context_get",
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
-           "pii_last_timings_ex", "pii_last_queue_sizes", "pii_window_enable", "pii_window_reset",
+           "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device"]
 
 
@@ -87,6 +87,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_last_timings.argtypes = [P, c.POINTER(c.c_float)]
     lib.pii_last_timings_ex.argtypes = [P, c.POINTER(c.c_float), c.c_uint32]
     lib.pii_last_queue_sizes.argtypes = [P, U64, U64]
+    lib.pii_last_stats.argtypes = [P, U64, c.c_uint32]
     lib.pii_window_enable.argtypes = [P, c.c_uint32, c.c_uint32]
     lib.pii_window_reset.argtypes = [P, c.c_uint32]
     lib.pii_window_count.argtypes = [P, c.c_uint32, U32]
@@ -267,6 +268,15 @@ class Engine:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         self.lib.pii_last_queue_sizes(self.h, ctypes.byref(a), ctypes.byref(b))
         return int(a.value), int(b.value)
+
+    def stats(self) -> dict:
+        """work sizes of the last call (pii_last_stats)"""
+        a = (ctypes.c_uint64 * 6)()
+        n = self.lib.pii_last_stats(self.h, a, 6)
+        if n < 0:
+            raise self._err(n, "pii_last_stats")
+        keys = ["pairs", "events", "lanes", "lane_bytes", "window_findings_arena", "spans"]
+        return {k: int(a[i]) for i, k in enumerate(keys[:n])}
 
     # ------------------------------------------------------------------ context + histogram
     def context_get(self, slot: int) -> Tuple[int, int]:

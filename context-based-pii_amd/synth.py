@@ -304,3 +304,14 @@ def gather_bytes(meta: CorpusMeta, bank: Bank, lo: int = 0, hi: int = None) -> n
 def make_corpus(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, conv_base: int = 0) -> Corpus:
     m = corpus_meta(n_conv, utt_per_conv, bank, seed, conv_base)
     return Corpus(gather_bytes(m, bank), m.offsets, m.conv_slot, m.role, m.ts_us, m.bank_id)
+
+
+def step_major(meta: CorpusMeta, bank: Bank, n_conv: int, utt_per_conv: int) -> CorpusMeta:
+    """The same rows streamed the way the aggregator sees them (config 3): step k = the k-th
+    utterance of every conversation, so rows [k*n_conv, (k+1)*n_conv) are one re-scan call."""
+    perm = (np.arange(utt_per_conv)[:, None] + utt_per_conv * np.arange(n_conv)[None, :]).reshape(-1)
+    bid = meta.bank_id[perm]
+    lens = (bank.offsets[1:] - bank.offsets[:-1])[bid]
+    offs = np.zeros(len(bid) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return CorpusMeta(bid, offs, meta.conv_slot[perm], meta.role[perm], meta.ts_us[perm])

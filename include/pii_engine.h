@@ -129,6 +129,10 @@ int pii_last_timings_ex(struct pii_engine* e, float* ms, uint32_t n);
 /* sizes of the last call's internal work queues: (start, pattern) candidate pairs and SCAN events
  * (what the roofline accounting of k_scan counts as written) */
 int pii_last_queue_sizes(struct pii_engine* e, uint64_t* pairs, uint64_t* events);
+/* the last call's work sizes: [0] candidate pairs [1] scan events [2] scan lanes [3] bytes per scan lane
+ * (1 KiB for big batches, down to 128 B for small ones) [4] window-findings arena entries [5] spans;
+ * fills min(n, 6) entries and returns that count */
+int pii_last_stats(struct pii_engine* e, uint64_t* out, uint32_t n);
 
 /* ---------------------------------------------------------------- multi-turn window re-scan (a12)
  * Replaces the aggregator's sliding-window re-scan (README.md:131-134, 159-168: keep the last N
