@@ -1148,6 +1148,120 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = bsum[gridDim.x];
 }
 
+// Single-pass exclusive scan (decoupled look-back): out[i] = in[0] + ... + in[i-1], out[n] = total.
+// A workgroup takes the next tile by ticket (so it only ever waits on tiles that are already running),
+// publishes its aggregate, then walks back over predecessors' published words until an inclusive
+// prefix.  A tile word is one 64-bit atomic: [epoch:24][status:2][value:38]; the epoch tells this
+// launch's words from stale ones, so the state array is never cleared.  ctr[0] = ticket counter,
+// ctr[1] = finished workgroups: the last one to finish zeroes both for the next launch.
+constexpr int LB_BLOCK = 256, LB_ITEMS = 16, LB_TILE = LB_BLOCK * LB_ITEMS;
+constexpr uint64_t LB_AGG = 1, LB_INCL = 2;
+
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t status, uint64_t v) {
+    return ((uint64_t)(epoch & 0xffffffu) << 40) | (status << 38) | (v & ((1ull << 38) - 1));
+}
+
+__global__ __launch_bounds__(LB_BLOCK) void k_scan_lb(const uint32_t* __restrict__ in, uint32_t n,
+                                                      uint64_t* __restrict__ out, unsigned long long* state,
+                                                      unsigned long long* ctr, uint32_t epoch) {
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_prefix;
+    __shared__ uint64_t s_w[LB_BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) s_tile = (uint32_t)atomicAdd(&ctr[0], 1ull);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t i0 = (uint64_t)tile * LB_TILE + (uint64_t)tid * LB_ITEMS;
+    uint32_t v[LB_ITEMS];
+    if (i0 + LB_ITEMS <= n && ((uintptr_t)(in + i0) & 15) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(in + i0);
+#pragma unroll
+        for (int k = 0; k < LB_ITEMS / 4; ++k) {
+            const uint4 x = p[k];
+            v[4 * k] = x.x;
+            v[4 * k + 1] = x.y;
+            v[4 * k + 2] = x.z;
+            v[4 * k + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < LB_ITEMS; ++k) v[k] = i0 + k < n ? in[i0 + k] : 0u;
+    }
+    uint64_t tsum = 0;
+#pragma unroll
+    for (int k = 0; k < LB_ITEMS; ++k) tsum += v[k];
+    uint64_t incl = tsum;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint64_t wpre = 0, total = 0;
+    for (int w = 0; w < LB_BLOCK / 64; ++w) {
+        if (w < wid) wpre += s_w[w];
+        total += s_w[w];
+    }
+    if (wid == 0) {
+        // wavefront 0: publish, then look back 64 predecessors at a time (one word per lane)
+        uint64_t prefix = 0;
+        if (tile == 0) {
+            if (lane == 0)
+                __hip_atomic_store(&state[0], lb_word(epoch, LB_INCL, total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&state[tile], lb_word(epoch, LB_AGG, total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t top = (int64_t)tile - 1;               // nearest predecessor of this window
+            for (;;) {
+                const int64_t j = top - lane;
+                uint64_t w = 0, st = LB_INCL, val = 0;     // lanes past tile 0 act as a zero inclusive word
+                if (j >= 0) {
+                    w = __hip_atomic_load(&state[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    st = ((uint32_t)(w >> 40) == (epoch & 0xffffffu)) ? (w >> 38) & 3 : 0;
+                    val = w & ((1ull << 38) - 1);
+                }
+                const uint64_t incl_mask = __ballot(st == LB_INCL);
+                const uint64_t ready = __ballot(st != 0);
+                // the nearest inclusive word ends the walk; every word before it must be ready
+                const int stop = incl_mask ? __builtin_ctzll(incl_mask) : 64;
+                const uint64_t need = stop == 64 ? ~0ull : ((2ull << stop) - 1);
+                if ((ready & need) != need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t x = lane <= stop ? val : 0;
+                for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
+                prefix += x;
+                if (stop < 64) break;
+                top -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&state[tile], lb_word(epoch, LB_INCL, prefix + total), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_prefix = prefix;
+    }
+    __syncthreads();
+    uint64_t run = s_prefix + wpre + incl - tsum;
+    if (i0 + LB_ITEMS <= n) {
+#pragma unroll
+        for (int k = 0; k < LB_ITEMS; ++k) {
+            out[i0 + k] = run;
+            run += v[k];
+        }
+    } else {
+        for (int k = 0; k < LB_ITEMS; ++k) {
+            if (i0 + k < n) out[i0 + k] = run;
+            run += v[k];
+        }
+    }
+    if (tile == gridDim.x - 1 && tid == 0) out[n] = s_prefix + total;
+    if (tid == 0 && atomicAdd(&ctr[1], 1ull) == gridDim.x - 1) {
+        ctr[0] = 0;
+        ctr[1] = 0;
+    }
+}
+
 __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t* __restrict__ span_offs,
                            uint32_t n_utt, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
                            uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count,
@@ -1436,11 +1550,14 @@ __global__ __launch_bounds__(256) void k_hist_reduce(const uint32_t* __restrict_
 constexpr int WN_MAX = 8;          // largest window (utterances)
 constexpr int WIN_TILE = 64;       // windows per k_win_redact workgroup
 
+constexpr int WHOT_BITS = 16;      // hotword rules whose proximity results are kept resident
 struct WCand {          // one resident candidate (16 B)
     uint32_t s, e;      // match [s, e), relative to its utterance
-    uint16_t p;         // detector pattern
+    uint8_t p;          // detector pattern
+    uint8_t need;       // predecessors its longest before-window needs (0: it stays inside the utterance)
+    uint16_t hot;       // bit h: hotword rule h hits, proximity windows clipped to the utterance
+    uint16_t hotx;      // bit h: ... before-window over the (up to `need`) preceding utterances
     uint16_t pad;
-    uint32_t hot;       // bit h: hotword rule h hits inside the utterance (windows clipped to it)
 };
 struct WDesc {          // one resident utterance of a conversation's history ring (16 B)
     uint32_t off;       // arena offset (16-aligned): nc WCands, then the text bytes
@@ -1705,14 +1822,68 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         WCand C;
         C.s = (uint32_t)s;
         C.e = (uint32_t)e;
-        C.p = (uint16_t)p;
+        C.p = (uint8_t)p;
+        C.need = 0;
+        C.hot = (uint16_t)phot[base + i];
+        C.hotx = C.hot;
         C.pad = 0;
-        C.hot = phot[base + i];
         wc[base + k++] = C;
     }
     if (u != 0xffffffffu && k > uf) {
         wc_first[u] = (uint32_t)(base + uf);
         wc_n[u] = k - uf;
+    }
+}
+
+// per NEW row: the before-windows of its candidates that reach across the "\n" into the preceding
+// utterances are evaluated ONCE, here, over the predecessors the row's own window holds (those are
+// the only ones any later window can hold before it): hotx + need.  A later window in which the
+// utterance has j >= need predecessors reuses hotx; j == 0 (window start) reuses hot.
+__global__ __launch_bounds__(256) void k_win_halo(const uint4* __restrict__ img, const LdsImage li, const WinRing W,
+                                                  const WinBatch B, WCand* __restrict__ wc,
+                                                  const uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    if (*err & (ERR_QUEUE | ERR_SLOT)) return;
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
+    const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
+    const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
+    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[EV_DTYPE]);
+    const uint32_t* thot = reinterpret_cast<const uint32_t*>(lb + li.off[EV_THOT]);
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= B.n_utt) return;
+    const uint32_t nc = B.wc_n[u];
+    if (nc == 0) return;
+    const WinIt it = win_begin(W, B, u);
+    const int j = it.nw - 1;                       // predecessors available
+    if (j == 0) return;
+    WCand* cl = wc + B.wc_first[u];
+    uint32_t oj = 0;                                // window offset of row u
+    for (int q = 0; q < j; ++q) oj += win_at(W, B, it, q).len + 1;
+    for (uint32_t k = 0; k < nc; ++k) {
+        WCand C = cl[k];
+        uint32_t mask = thot[dtype[C.p]] & ((1u << WHOT_BITS) - 1);
+        int wbmax = 0;
+        for (uint32_t m = mask; m; m &= m - 1) wbmax = max(wbmax, hrule[4 * __builtin_ctz(m)]);
+        if ((int)C.s >= wbmax) continue;
+        // predecessors the longest before-window reaches (all available ones if it reaches past them)
+        int need = 0;
+        uint32_t cover = C.s;
+        while (need < j && cover < (uint32_t)wbmax) {
+            ++need;
+            cover += win_at(W, B, it, j - need).len + 1;
+        }
+        uint32_t hx = C.hot;
+        const uint32_t ps = oj + C.s;
+        for (uint32_t m = mask & ~(uint32_t)C.hot; m; m &= m - 1) {
+            const int h = __builtin_ctz(m);
+            const int wb = hrule[4 * h];
+            if (wb > 0 && (int)C.s < wb && hot_run_win(pool, hdesc + 8 * h, W, B, it, ps > (uint32_t)wb ? ps - wb : 0u, ps))
+                hx |= 1u << h;
+        }
+        C.need = (uint8_t)need;
+        C.hotx = (uint16_t)hx;
+        cl[k] = C;
     }
 }
 
@@ -1813,18 +1984,20 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
             if (!ven[v * T + t]) continue;
             int lik = dlik[p];
             const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
+            // resident proximity bits: at the window start the clipped ones, with >= need predecessors
+            // the ones over the halo; otherwise (or for rules past WHOT_BITS) re-run over the window
+            const bool known = C.need == 0 || j == 0 || j >= (int)C.need;
+            const uint32_t bits = (C.need == 0 || j == 0) ? C.hot : C.hotx;
             for (uint32_t q = r0; q < r1; ++q) {
                 const int h = rids[q];
                 const int wb = hrule[4 * h], wa = hrule[4 * h + 1];
-                const bool cb = wb > 0 && s < wb && j > 0;                       // reaches the previous utterance
-                const bool ca = wa > 0 && (uint32_t)(e + wa) > Ej.len && j + 1 < nw;   // reaches the next one
+                const bool ca = wa > 0 && (uint32_t)(e + wa) > Ej.len && j + 1 < nw;   // reaches the next utterance
+                const uint32_t ps = oj + (uint32_t)s, pe = oj + (uint32_t)e;
                 bool hit;
-                if (h < 32 && ((C.hot >> h) & 1u)) {
-                    hit = true;                                                 // inside the utterance
-                } else if (h < 32 && !cb && !ca) {
-                    hit = false;
+                if (h < WHOT_BITS && known) {
+                    hit = (bits >> h) & 1u;
+                    if (!hit && ca) hit = hot_run_win(pool, hdesc + 8 * h, W, B, it, pe, min(WL, pe + (uint32_t)wa));
                 } else {
-                    const uint32_t ps = oj + (uint32_t)s, pe = oj + (uint32_t)e;
                     hit = wb > 0 && hot_run_win(pool, hdesc + 8 * h, W, B, it, ps > (uint32_t)wb ? ps - wb : 0u, ps);
                     if (!hit && wa > 0) hit = hot_run_win(pool, hdesc + 8 * h, W, B, it, pe, min(WL, pe + (uint32_t)wa));
                 }
@@ -2250,6 +2423,8 @@ struct pii_engine {
     int16_t *kw = nullptr, *ctx = nullptr;
     int32_t *agg_v = nullptr, *commit = nullptr;
     uint64_t *span_offs = nullptr, *bsum = nullptr, *out_offs_tmp = nullptr;
+    unsigned long long *lb_state = nullptr, *lb_ticket = nullptr;   // single-pass scan tiles / ticket counter
+    uint32_t lb_cap = 0, lb_epoch = 0;
     uint32_t* d_err = nullptr;
     uint64_t* d_totals = nullptr;
     uint64_t* h_totals = nullptr;
@@ -2367,15 +2542,34 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
     return rc;
 }
 
+// Small scans (a re-scan step: ~100k rows) take the single-pass look-back kernel, one launch instead
+// of three; big ones (10M rows) the reduce / scan-of-sums / apply triple, whose tiles never wait on
+// each other (the look-back's cross-XCD hand-offs chain up over thousands of tiles: 0.4 ms vs 0.06).
+constexpr uint32_t LB_MAX_TILES = 64;
+
 int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out, hipStream_t st) {
-    const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint32_t nb = (n + LB_TILE - 1) / LB_TILE;
     if (nb == 0) {
         HIPCHK(hipMemsetAsync(out, 0, sizeof(uint64_t), st));
         return PII_OK;
     }
-    k_scan_reduce<<<nb, 256, 0, st>>>(in, n, e->bsum);
-    k_scan_blocks<<<1, 256, 0, st>>>(e->bsum, nb);
-    k_scan_apply<<<nb, 256, 0, st>>>(in, n, e->bsum, out);
+    if (nb > LB_MAX_TILES) {
+        const uint32_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+        k_scan_reduce<<<nt, 256, 0, st>>>(in, n, e->bsum);
+        k_scan_blocks<<<1, 256, 0, st>>>(e->bsum, nt);
+        k_scan_apply<<<nt, 256, 0, st>>>(in, n, e->bsum, out);
+        HIPCHK(hipGetLastError());
+        return PII_OK;
+    }
+    if (nb > e->lb_cap) {
+        int rc = grow(e, e->lb_state, (size_t)nb + 64);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(e->lb_state, 0, ((size_t)nb + 64) * 8, st));
+        e->lb_cap = nb + 64;
+    }
+    e->lb_epoch = (e->lb_epoch + 1) & 0xffffffu;
+    if (e->lb_epoch == 0) e->lb_epoch = 1;
+    k_scan_lb<<<nb, LB_BLOCK, 0, st>>>(in, n, out, e->lb_state, e->lb_ticket, e->lb_epoch);
     HIPCHK(hipGetLastError());
     return PII_OK;
 }
@@ -2575,10 +2769,12 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
                                                             e->wc_n, e->d_err);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[3], st));
     const WinRing W{e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->win_n, e->win_slot_bytes, e->n_slots, 0};
     const WinBatch B{text, offs, slot, e->wc, e->wc_first, e->wc_n, n_utt};
     const uint32_t nb = (n_utt + 255) / 256;
+    if (n_utt > 0 && n_chunks > 0)
+        k_win_halo<<<nb, 256, e->img_eval.li.total, st>>>(e->img_eval.d, e->img_eval.li, W, B, e->wc, e->d_err);
+    HIPCHK(hipEventRecord(e->tev[3], st));
     if (n_utt > 0) {
         k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
         if ((rc = exclusive_scan(e, e->wbound, n_utt, e->wfbase, st))) return rc;
@@ -2839,7 +3035,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             for (int v = 0; v < R.V; ++v)
                 for (int t = 0; t < R.T; ++t)
                     for (uint32_t q = ro[v * R.T + t]; q < ro[v * R.T + t + 1]; ++q)
-                        if (ri[q] < 32) thot[t] |= 1u << ri[q];
+                        if (ri[q] < 32) thot[t] |= 1u << ri[q];     // k_win_* cache the first WHOT_BITS
         }
         pe[EV_THOT] = vec(thot);
         std::vector<std::pair<const void*, size_t>> pw(WS_N);
@@ -2870,7 +3066,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first, &e->img_first}, {(const void*)k_pair_eval, &e->img_eval},
             {(const void*)k_select, &e->img_sel}, {(const void*)k_win_eval, &e->img_eval},
-            {(const void*)k_win_select, &e->img_wsel}};
+            {(const void*)k_win_select, &e->img_wsel}, {(const void*)k_win_halo, &e->img_eval}};
         for (auto& kb : big)
             if (kb.second->li.total > 64 * 1024 &&
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
@@ -2897,7 +3093,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
         hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, 256 * 8) != hipSuccess ||
         hipMalloc(&e->d_err, 16) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
-        hipMalloc(&e->pair_count, 16) != hipSuccess)
+        hipMalloc(&e->pair_count, 16) != hipSuccess || hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
+        hipMemset(e->lb_ticket, 0, 16) != hipSuccess)
         return fail("state allocation failed");
     if (hipHostMalloc(&e->h_totals, 64) != hipSuccess) return fail("pinned allocation failed");
     std::vector<int32_t> g(ns, -1);
@@ -2917,7 +3114,7 @@ int pii_engine_destroy(pii_engine* e) {
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
                     e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
-                    e->span_offs, e->bsum, e->out_offs_tmp, e->d_err, e->d_totals, e->h_text, e->h_role,
+                    e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd};

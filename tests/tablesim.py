@@ -188,12 +188,19 @@ class TableSim:
                 hs.add(int(self.rule_ids[k]))
         return sorted(hs)
 
-    def resident_cands(self, text: bytes):
-        """Variant-independent candidates of one utterance, as k_win_eval + k_win_cands build them:
-        finditer per pattern, validator-passing, inner hotword bits (windows clipped to the text)."""
+    WHOT_BITS = 16
+
+    def resident_cands(self, text: bytes, preds=()):
+        """Variant-independent candidates of one utterance, as k_win_eval + k_win_cands + k_win_halo
+        build them: finditer per pattern, validator-passing, hotword bits with the proximity windows
+        clipped to the text (hot) and with the before-window over the preceding utterances `preds`
+        (oldest first, the ones the utterance's own window holds) (hotx), and `need` = predecessors
+        the longest before-window reaches."""
         events = self.scan(text, agent=False)
         cur = [0] * self.P
         out = []
+        W = b"\n".join(list(preds) + [text])
+        oj = len(W) - len(text)
         for pos, sd, sk in sorted(events):
             cd, _ = self._classes(text, pos)
             a = int(self.dacc[sd, cd])
@@ -208,13 +215,26 @@ class TableSim:
                 val = int(self.det_val[p])
                 if val and not self.validators[val](text[pos:e]):
                     continue
+                hs = [h for h in self.type_hot_any(int(self.det_type[p])) if h < self.WHOT_BITS]
                 hot = 0
-                for h in self.type_hot_any(int(self.det_type[p])):
+                for h in hs:
                     wb, wa = int(self.hot_rule[h][0]), int(self.hot_rule[h][1])
                     if (wb > 0 and self.hot_run(h, text[max(0, pos - wb):pos])) or \
                             (wa > 0 and self.hot_run(h, text[e:e + wa])):
                         hot |= 1 << h
-                out.append((pos, e, p, hot))
+                hotx, need = hot, 0
+                wbmax = max([int(self.hot_rule[h][0]) for h in hs] or [0])
+                if preds and pos < wbmax:
+                    cover = pos
+                    while need < len(preds) and cover < wbmax:
+                        need += 1
+                        cover += len(preds[-need]) + 1
+                    ps = oj + pos
+                    for h in hs:
+                        wb = int(self.hot_rule[h][0])
+                        if not (hot >> h) & 1 and wb > 0 and pos < wb and self.hot_run(h, W[max(0, ps - wb):ps]):
+                            hotx |= 1 << h
+                out.append((pos, e, p, hot, hotx, need))
         return out
 
     def window_select(self, entries, v: int):
@@ -237,7 +257,7 @@ class TableSim:
                     _, (ss, e, t, lik) = best
                     kept.append((oj + ss, oj + e, t, lik))
                     max_end = oj + e
-            for (cs, e, p, hot) in cands:
+            for (cs, e, p, hot, hotx, need) in cands:
                 if cs != s:
                     flush()
                     best, s = None, cs
@@ -245,17 +265,16 @@ class TableSim:
                 if not self.enabled[v, t]:
                     continue
                 lik = int(self.det_lik[p])
+                known = need == 0 or j == 0 or j >= need
+                bits = hot if (need == 0 or j == 0) else hotx
                 for k in range(int(self.rule_off[v * self.T + t]), int(self.rule_off[v * self.T + t + 1])):
                     h = int(self.rule_ids[k])
                     wb, wa, fixed, rel = [int(x) for x in self.hot_rule[h]]
-                    cb = wb > 0 and s < wb and j > 0
                     ca = wa > 0 and e + wa > len(text) and j + 1 < nw
-                    if (hot >> h) & 1:
-                        hit = True
-                    elif not cb and not ca:
-                        hit = False
+                    ps, pe = oj + s, oj + e
+                    if h < self.WHOT_BITS and known:
+                        hit = bool((bits >> h) & 1) or (ca and self.hot_run(h, W[pe:pe + wa]))
                     else:
-                        ps, pe = oj + s, oj + e
                         hit = (wb > 0 and self.hot_run(h, W[max(0, ps - wb):ps])) or \
                               (wa > 0 and self.hot_run(h, W[pe:pe + wa]))
                     if hit:

@@ -19,10 +19,13 @@ def sim(compiled):
     return TableSim(compiled)
 
 
-def _windows_equal(sim, oracle_cfg, texts, et):
+def _windows_equal(sim, oracle_cfg, texts, et, history=()):
+    """texts = the window; `history` = utterances before it (they shaped the residents' halo bits)"""
     from oracle import pii_oracle as O
     v = 0 if et is None else 1 + list(oracle_cfg.context_keywords.keys()).index(et)
-    entries = [(t, sim.resident_cands(t)) for t in texts]
+    conv = list(history) + list(texts)
+    n0 = len(history)
+    entries = [(conv[i], sim.resident_cands(conv[i], conv[max(0, i - 4):i])) for i in range(n0, len(conv))]
     W, kept = sim.window_select(entries, v)
     red, fs = O.redact(W, oracle_cfg, et)
     assert sim.redact(W, kept) == red, (texts, et)
@@ -41,6 +44,9 @@ def test_hotword_halo_across_utterances(sim, oracle_cfg):
         _windows_equal(sim, oracle_cfg, [b"ok", b"what's your driver's license", b"",
                                          b"G223456789", b"and passport E98765432"], et)
         _windows_equal(sim, oracle_cfg, [b"card number", b"\n", b"4141 1212 2323 5009"], et)
+        # the hotword sat in an utterance that has left the window: the resident halo bits must not leak
+        _windows_equal(sim, oracle_cfg, [b"x", b"987654321 thanks"], et, history=[b"your social security"])
+        _windows_equal(sim, oracle_cfg, [b"987654321 thanks"], et, history=[b"ssn", b"is"])
 
 
 def test_window_random_synthetic(sim, oracle_cfg):
@@ -50,13 +56,14 @@ def test_window_random_synthetic(sim, oracle_cfg):
     rng = random.Random(4)
     groups = [None] + list(oracle_cfg.context_keywords.keys())
     texts = [corp.data[int(corp.offsets[i]):int(corp.offsets[i + 1])].tobytes() for i in range(corp.n)]
-    for _ in range(150):
+    for _ in range(200):
         n = rng.randint(1, 5)
-        i = rng.randrange(0, len(texts) - n)
-        win = texts[i:i + n]
-        if rng.random() < 0.3:                      # short rows: hotword windows span several rows
-            win = [w[-rng.randint(0, 30):] if w else w for w in win]
-        _windows_equal(sim, oracle_cfg, win, rng.choice(groups))
+        i = rng.randrange(0, len(texts) - n - 4)
+        conv = texts[i:i + n + 4]
+        if rng.random() < 0.4:                      # short rows: hotword windows span several rows
+            conv = [w[-rng.randint(0, 30):] if w else w for w in conv]
+        h = rng.randint(0, 4)                        # utterances already dropped from the window
+        _windows_equal(sim, oracle_cfg, conv[h:h + n], rng.choice(groups), history=conv[:h])
 
 
 def test_process_window_rows_context(oracle_cfg):
