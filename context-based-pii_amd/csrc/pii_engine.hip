@@ -57,14 +57,16 @@ struct Event {
 struct RulesDev {
     int P, G, T, V, SD, CD, d_start, SK, CK, k_start, n_hot, min_len;
     int kw_always_min, NE;
+    int CDs, CKs;                // row strides of the SCAN tables (CD / CK rounded up to even)
     uint32_t n_dacc, n_kacc;     // D / K accept sets
     const uint32_t* cmap4;    // [256] 2*classD | 2*classK << 16 (byte offsets)
-    const uint16_t* td;       // [SD*CD] LDS byte address of the next row in k_scan | accept (bit 0)
-    const uint16_t* tk;       // [SK*CK]
-    const uint16_t* d_accid;  // [SD*CD]
+    const uint16_t* td;       // [SD*CDs] LDS byte address of the next row in k_scan | accept (bit 0)
+                              //   | the next row's end-of-text transition accepts (bit 1)
+    const uint16_t* tk;       // [SK*CKs]
+    const uint16_t* d_accid;  // [SD*CDs]
     const uint32_t* d_acc_off;
     const uint16_t* d_acc_ids;
-    const uint16_t* k_accid;  // [SK*CK]
+    const uint16_t* k_accid;  // [SK*CKs]
     const uint16_t* k_acc_min;  // per K accept set: smallest context group
     const uint16_t* det_type;
     const uint8_t* det_val;
@@ -230,19 +232,6 @@ __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt,
     }
 }
 
-// utterance start at pos: the end-of-text pseudo step, then reset
-__device__ __forceinline__ void scan_bot(const uint8_t* lds, uint32_t eot_d, uint32_t eot_k, uint32_t d_start,
-                                         uint32_t k_start, uint32_t tk_base, uint32_t& sd, uint32_t& sk,
-                                         uint32_t& cnt, Event* __restrict__ ev, uint32_t pos, uint32_t lo_r,
-                                         uint32_t len_r) {
-    (void)lds;
-    const uint32_t nd = lds_u16(sd + eot_d);
-    const uint32_t nk = lds_u16(sk + eot_k);
-    if ((nd | nk) & 1u) scan_emit(ev, cnt, pos, lo_r, len_r, sd + eot_d, sk + eot_k, tk_base);
-    sd = d_start;
-    sk = k_start;
-}
-
 // byte classes of 8 bytes (HALF = 0: bytes 8..15 of the chunk, 1: bytes 0..7), issued together
 #define SCAN_CLASSES8(W, H)                                                                       \
     cc[0] = s_cmap[byte_c<(H) + 0>(W)];                                                           \
@@ -255,18 +244,24 @@ __device__ __forceinline__ void scan_bot(const uint8_t* lds, uint32_t eot_d, uin
     cc[7] = s_cmap[byte_c<(H) + 7>(W)];
 
 // SCAN_STEP reads cc[K] for K in 0..15; with 8 classes in flight it is invoked with K - H
+// An utterance start (bit of b16) resets both automata without a branch: the end-of-text step's
+// accept is bit 1 of the entry just read (the destination row's EOT transition), so only an
+// event (accept on the byte, or on EOT at a reset) leaves the straight-line path.
 #define SCAN_STEP8(J, H, OFF)                                                                     \
     {                                                                                             \
         const uint32_t ad = sd + (cc[J] & 0xffffu);                                               \
         const uint32_t ak = sk + (cc[J] >> 16);                                                   \
         const uint32_t nd = lds_u16(ad);                                                          \
         const uint32_t nk = lds_u16(ak);                                                          \
-        sd = nd & 0xfffeu;                                                                        \
-        sk = nk & 0xfffeu;                                                                        \
-        if (__builtin_expect((((nd | nk) & 1u) | (b16 & (1u << ((H) + (J))))) != 0, 0)) {         \
-            if ((nd | nk) & 1u) scan_emit(ev, cnt, bpos + (OFF) + (H) + (J) + 1, lo_r, len_r, ad, ak, tk_base); \
-            if (b16 & (1u << ((H) + (J))))                                                        \
-                scan_bot(lds, eot_d, eot_k, d_start, k_start, tk_base, sd, sk, cnt, ev, bpos + (OFF) + (H) + (J), lo_r, len_r); \
+        const uint32_t rs = (b16 >> ((H) + (J))) & 1u;                                            \
+        const uint32_t nn = nd | nk;                                                              \
+        sd = rs ? d_start : (nd & 0xfffcu);                                                       \
+        sk = rs ? k_start : (nk & 0xfffcu);                                                       \
+        if (__builtin_expect((nn & (1u | (rs << 1))) != 0, 0)) {                                  \
+            if (nn & 1u) scan_emit(ev, cnt, bpos + (OFF) + (H) + (J) + 1, lo_r, len_r, ad, ak, tk_base); \
+            if (rs & (nn >> 1))                                                                   \
+                scan_emit(ev, cnt, bpos + (OFF) + (H) + (J), lo_r, len_r, (nd & 0xfffcu) + eot_d, \
+                          (nk & 0xfffcu) + eot_k, tk_base);                                       \
         }                                                                                         \
     }
 
@@ -289,9 +284,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
                                                      uint32_t* __restrict__ lane_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
-    const int nd_words = (R.SD * R.CD + 1) / 2;
-    const int nk_words = (R.SK * R.CK + 1) / 2;
-    const uint8_t* lds = reinterpret_cast<const uint8_t*>(smem32);
+    const int nd_words = R.SD * R.CDs / 2;      // rows padded to an even class count
+    const int nk_words = R.SK * R.CKs / 2;
     const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)nd_words * 4;
     {
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
@@ -2867,8 +2861,12 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         return PII_E_RULES;
     };
     if (R.P > P_MAX) return fail("more detector patterns than P_MAX");
-    // scan table entries are 16-bit LDS byte addresses (k_scan layout: class map, D rows, K rows)
-    const uint32_t td_words = (uint32_t)((R.SD * R.CD + 1) / 2), tk_words = (uint32_t)((R.SK * R.CK + 1) / 2);
+    // scan table entries are 16-bit LDS byte addresses (k_scan layout: class map, D rows, K rows);
+    // rows are padded to an even class count so every row address is a multiple of 4 and bit 1 of
+    // an entry is free for the destination's end-of-text accept
+    R.CDs = (R.CD + 1) & ~1;
+    R.CKs = (R.CK + 1) & ~1;
+    const uint32_t td_words = (uint32_t)(R.SD * R.CDs / 2), tk_words = (uint32_t)(R.SK * R.CKs / 2);
     const uint32_t tk_base = SCAN_TD_BASE + td_words * 4;
     if ((uint64_t)tk_base + (uint64_t)tk_words * 4 > 65536) return fail("SCAN tables exceed 64 KiB of LDS");
     if (R.T > 65535) return fail("too many types");
@@ -2890,17 +2888,30 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         for (int g = 0; g < R.G; ++g) e->kw_type.push_back(k[g]);
     }
     // host-side derived tables
-    std::vector<uint16_t> td(R.SD * R.CD), tk(R.SK * R.CK);
+    std::vector<uint16_t> td(R.SD * R.CDs, 0), tk(R.SK * R.CKs, 0), dacc(R.SD * R.CDs, 0), kacc(R.SK * R.CKs, 0);
     {
-        const uint16_t* s = reinterpret_cast<const uint16_t*>(find("scan.d.trans")->data);
-        for (int i = 0; i < R.SD * R.CD; ++i)
-            td[i] = (uint16_t)((SCAN_TD_BASE + (s[i] & 0x7fff) * R.CD * 2) | (s[i] >> 15));
-        const uint16_t* k = reinterpret_cast<const uint16_t*>(find("scan.k.trans")->data);
-        for (int i = 0; i < R.SK * R.CK; ++i)
-            tk[i] = (uint16_t)((tk_base + (k[i] & 0x7fff) * R.CK * 2) | (k[i] >> 15));
+        // entry (row, class) = address of the destination row | accept | accept of the destination's
+        // end-of-text transition (class C-1) << 1, so k_scan resets at an utterance start without
+        // reading the end-of-text entry
+        auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, uint32_t base,
+                           uint16_t* t, uint16_t* a) {
+            for (int r = 0; r < S; ++r)
+                for (int c = 0; c < C; ++c) {
+                    const uint32_t v = s[r * C + c], dst = v & 0x7fff;
+                    const uint32_t eot = s[dst * C + C - 1] >> 15;
+                    t[r * Cs + c] = (uint16_t)((base + dst * Cs * 2) | (v >> 15) | (eot << 1));
+                    a[r * Cs + c] = acc[r * C + c];
+                }
+        };
+        relayout(reinterpret_cast<const uint16_t*>(find("scan.d.trans")->data),
+                 reinterpret_cast<const uint16_t*>(find("scan.d.accid")->data), R.SD, R.CD, R.CDs, SCAN_TD_BASE,
+                 td.data(), dacc.data());
+        relayout(reinterpret_cast<const uint16_t*>(find("scan.k.trans")->data),
+                 reinterpret_cast<const uint16_t*>(find("scan.k.accid")->data), R.SK, R.CK, R.CKs, tk_base,
+                 tk.data(), kacc.data());
     }
-    R.d_start = (int)(SCAN_TD_BASE + R.d_start * R.CD * 2);     // start rows as LDS byte addresses
-    R.k_start = (int)(tk_base + R.k_start * R.CK * 2);
+    R.d_start = (int)(SCAN_TD_BASE + R.d_start * R.CDs * 2);     // start rows as LDS byte addresses
+    R.k_start = (int)(tk_base + R.k_start * R.CKs * 2);
     std::vector<uint32_t> cmap4(256);
     {
         const uint16_t* c2 = reinterpret_cast<const uint16_t*>(find("scan.cmap2")->data);
@@ -2962,8 +2973,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     };
     auto addsec = [&](const char* nm) { return add(find(nm)->data, find(nm)->bytes); };
     size_t i_cmap = add(cmap4.data(), cmap4.size() * 4), i_td = add(td.data(), td.size() * 2), i_tk = add(tk.data(), tk.size() * 2);
-    size_t i_dacc = addsec("scan.d.accid"), i_doff = addsec("scan.d.acc_off"), i_dids = addsec("scan.d.acc_ids");
-    size_t i_kacc = addsec("scan.k.accid"), i_kmin = add(k_acc_min.data(), k_acc_min.size() * 2);
+    size_t i_dacc = add(dacc.data(), dacc.size() * 2), i_doff = addsec("scan.d.acc_off"), i_dids = addsec("scan.d.acc_ids");
+    size_t i_kacc = add(kacc.data(), kacc.size() * 2), i_kmin = add(k_acc_min.data(), k_acc_min.size() * 2);
     size_t i_dt = addsec("det.type"), i_dv = addsec("det.validator"), i_dl = addsec("det.lik"),
            i_dx = addsec("det.exidx"), i_fd = addsec("det.first_desc"), i_hr = addsec("hot.rule"),
            i_hd = addsec("hot.dfa_desc"), i_ve = addsec("var.enabled"), i_vm = addsec("var.minlik"),
@@ -3078,7 +3089,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
-    e->scan_lds = 1024 + (size_t)((R.SD * R.CD + 1) / 2) * 4 + (size_t)((R.SK * R.CK + 1) / 2) * 4;
+    e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     if (e->scan_lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess)

@@ -21,6 +21,13 @@ the realtime handler reads it) and lives beside the slot map; its expiry follows
 
 Throughput path: ``process_batch`` runs many rows in one engine call (the batch contract of
 include/pii_engine.h: a conversation's rows contiguous and in entry order).
+
+Aggregator path (transcript_aggregator_service, README.md:131-134, 159-168): ``rescan_window_batch``
+appends each row to its conversation's window of the last N utterances (N = 5,
+transcript_aggregator_service/cloudbuild.yaml:33) and returns the redacted "\\n"-joined window, the
+re-scan the README describes; ``conversation_ended`` drops a conversation's window (the
+``/conversation-ended`` endpoint, transcript_aggregator_service/main.py).  The window lives in HBM
+(pii_rescan_window); only the new utterance is scanned.
 """
 from __future__ import annotations
 
@@ -116,6 +123,8 @@ class PiiService:
     def _evict(self, slot: int):
         self.engine.context_set(slot, -1, 0)
         self.agent_text.pop(slot, None)
+        if getattr(self.engine, "window_n", 0):
+            self.engine.window_reset(slot)
 
     def _context_record(self, slot: int, now_us: int) -> Optional[dict]:
         """The Redis record of main.py:366-374 as the reference's GET returns it (None when absent
@@ -203,6 +212,34 @@ class PiiService:
         else:
             redacted = self.call_dlp_for_redaction(utterance, rec)
         return {"redacted_utterance": redacted}, 200
+
+    # ---------------------------------------------------------------- aggregator re-scan (a12)
+    def rescan_window_batch(self, rows: Sequence[dict], window_n: int = 5, slot_bytes: int = 8192) -> List[str]:
+        """Rows as process_batch (original text) -> per row the redacted window
+        "\\n".join(last window_n utterances of its conversation), re-scanned with the conversation's
+        current expected_pii_type.  Agent rows update the context as handle_agent_utterance does."""
+        texts, slots, roles, ts = [], [], [], []
+        with self.lock:
+            if getattr(self.engine, "window_n", 0) == 0:
+                self.engine.window_enable(window_n, slot_bytes)
+            elif self.engine.window_n != window_n:
+                raise ValueError(f"window already enabled with N={self.engine.window_n}")
+            for r in rows:
+                texts.append(_enc(r["text"]))
+                slots.append(self.slots.get(r["conversation_id"]))
+                pr = str(r.get("participant_role", "")).upper()
+                roles.append(ROLE_AGENT if pr == "AGENT" else ROLE_CUSTOMER if pr in ("END_USER", "CUSTOMER")
+                             else ROLE_OTHER)
+                ts.append(int(r.get("start_timestamp_usec", self._now_us())))
+            res = self.engine.rescan_window(texts, slots, roles, ts)
+            return [_dec(res.text(i)) for i in range(len(rows))]
+
+    def conversation_ended(self, conversation_id) -> None:
+        """/conversation-ended: the conversation's window and context are dropped."""
+        with self.lock:
+            slot = self.slots.peek(conversation_id)
+            if slot is not None and getattr(self.engine, "window_n", 0):
+                self.engine.window_reset(slot)
 
     # ---------------------------------------------------------------- batched ingest
     def process_batch(self, rows: Sequence[dict]) -> List[str]:

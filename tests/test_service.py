@@ -189,3 +189,26 @@ def test_service_on_gpu_matches_oracle(oracle_cfg):
     body, _ = svc.redact_utterance_realtime({"conversation_id": "rt", "utterance": "sure 490154203237518"})
     assert body["redacted_utterance"] == O.realtime_redact(agent.encode(), b"sure 490154203237518", oracle_cfg,
                                                            O.extract_expected_pii(agent.encode(), oracle_cfg)).decode()
+
+
+@pytest.mark.gpu
+def test_service_window_rescan_on_gpu(oracle_cfg):
+    """The aggregator's re-scan (rescan_window_batch) over the golden transcripts streamed one
+    utterance per call, and in one batch, vs oracle.process_window_rows; conversation_ended resets."""
+    from oracle import pii_oracle as O
+    S = pkg("service")
+    svc = S.PiiService(n_slots=64, clock=Clock())
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    role = {"AGENT": O.ROLE_AGENT}
+    for mode in ("stream", "batch"):
+        for name, t in tr.items():
+            cid = mode + t["conversation_id"]
+            rows = [{"conversation_id": cid, "participant_role": e["role"], "text": e["text"],
+                     "start_timestamp_usec": e["ts"]} for e in t["entries"]]
+            exp = [r.decode() for r, _, _ in O.process_window_rows(
+                [(cid, role.get(e["role"], O.ROLE_CUSTOMER), e["text"].encode(), e["ts"]) for e in t["entries"]],
+                oracle_cfg, n=5)]
+            got = [svc.rescan_window_batch([r])[0] for r in rows] if mode == "stream" else svc.rescan_window_batch(rows)
+            assert got == exp, (mode, name)
+            svc.conversation_ended(cid)
+            assert svc.engine.window_count(svc.slots.peek(cid)) == 0
