@@ -34,12 +34,20 @@ __device__ __forceinline__ uint4 window16(const uint4& a, const uint4& b, uint32
 
 // bytes [src, src + 16) as a uint4, reading only the aligned 16-byte chunks that hold a byte of
 // [src + need_lo, src + need_hi) (so never a chunk outside the caller's buffer); other bytes are 0
+// Every caller passes a pointer into HBM (text, token bytes, window rings): the loads are issued as
+// global (address space 1), not flat -- a flat load also counts against lgkmcnt, so the next LDS
+// wait would stall on it.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4_t g_u32x4_t;
+__device__ __forceinline__ uint4 gload16(uintptr_t a) {      // 16-byte aligned global load
+    const u32x4_t v = *(g_u32x4_t*)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint4 load16(const uint8_t* src, int need_lo, int need_hi) {
     const uintptr_t a = (uintptr_t)src & ~(uintptr_t)15;
-    const uint4* p = reinterpret_cast<const uint4*>(a);
     uint4 x = make_uint4(0, 0, 0, 0), y = x;
-    if (a + 16 > (uintptr_t)(src + need_lo)) x = p[0];
-    if (a + 16 < (uintptr_t)(src + need_hi)) y = p[1];
+    if (a + 16 > (uintptr_t)(src + need_lo)) x = gload16(a);
+    if (a + 16 < (uintptr_t)(src + need_hi)) y = gload16(a + 16);
     return window16(x, y, (uint32_t)((uintptr_t)src - a));
 }
 

@@ -243,38 +243,70 @@ __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt,
     cc[6] = s_cmap[byte_c<(H) + 6>(W)];                                                           \
     cc[7] = s_cmap[byte_c<(H) + 7>(W)];
 
-// SCAN_STEP reads cc[K] for K in 0..15; with 8 classes in flight it is invoked with K - H
-// An utterance start (bit of b16) resets both automata without a branch: the end-of-text step's
-// accept is bit 1 of the entry just read (the destination row's EOT transition), so only an
-// event (accept on the byte, or on EOT at a reset) leaves the straight-line path.
-#define SCAN_STEP8(J, H, OFF)                                                                     \
+// v[j] for a per-lane j in 0..7 (a select tree: the arrays stay in registers)
+__device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t j) {
+    const bool b0 = j & 1u, b1 = j & 2u, b2 = j & 4u;
+    const uint32_t v01 = b0 ? v[1] : v[0], v23 = b0 ? v[3] : v[2];
+    const uint32_t v45 = b0 ? v[5] : v[4], v67 = b0 ? v[7] : v[6];
+    const uint32_t v03 = b1 ? v23 : v01, v47 = b1 ? v67 : v45;
+    return b2 ? v47 : v03;
+}
+
+// The events of one 8-byte group, in the order the per-step scan produced them (byte 7 first; on a
+// byte, its accept before the end-of-text accept of an utterance start).  m holds 2 flag bits per
+// byte j at bit 2 (7 - j): bit 0 = an automaton accepted on the byte (record its transitions ad[j],
+// ak[j], start pos + 1), bit 1 = the byte starts an utterance and the destination row accepts at
+// end of text (record the destination rows' EOT transitions, start pos).
+__device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt, uint32_t m,
+                                           const uint32_t (&ad)[8], const uint32_t (&ak)[8], uint32_t p0,
+                                           uint32_t lo_r, uint32_t len_r, uint32_t tk_base, uint32_t eot_d,
+                                           uint32_t eot_k) {
+    do {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        const uint32_t j = 7u - (b >> 1);
+        uint32_t a = sel8(ad, j), k = sel8(ak, j);
+        uint32_t pos = p0 + j + 1u;
+        if (b & 1u) {
+            a = (lds_u16(a) & 0xfffcu) + eot_d;
+            k = (lds_u16(k) & 0xfffcu) + eot_k;
+            pos -= 1u;
+        }
+        scan_emit(ev, cnt, pos, lo_r, len_r, a, k, tk_base);
+    } while (m);
+}
+
+// One byte of both reverse automata.  nd/nk are the raw entries of the previous step; pm is all ones
+// iff the previous byte started an utterance, and then the row becomes the start row without a
+// branch: (entry & ~pm & ~3) + (class + (pm & start)).  Rows and classes stay below 64 KiB, so the
+// packed class pair + packed start pair add without a carry between the halves.  The two dependent
+// ALU ops between LDS reads are the whole per-byte chain; flags go to m and are emitted per 8 bytes.
+#define SCAN_STEP8(J, H)                                                                          \
     {                                                                                             \
-        const uint32_t ad = sd + (cc[J] & 0xffffu);                                               \
-        const uint32_t ak = sk + (cc[J] >> 16);                                                   \
-        const uint32_t nd = lds_u16(ad);                                                          \
-        const uint32_t nk = lds_u16(ak);                                                          \
-        const uint32_t rs = (b16 >> ((H) + (J))) & 1u;                                            \
-        const uint32_t nn = nd | nk;                                                              \
-        sd = rs ? d_start : (nd & 0xfffcu);                                                       \
-        sk = rs ? k_start : (nk & 0xfffcu);                                                       \
-        if (__builtin_expect((nn & (1u | (rs << 1))) != 0, 0)) {                                  \
-            if (nn & 1u) scan_emit(ev, cnt, bpos + (OFF) + (H) + (J) + 1, lo_r, len_r, ad, ak, tk_base); \
-            if (rs & (nn >> 1))                                                                   \
-                scan_emit(ev, cnt, bpos + (OFF) + (H) + (J), lo_r, len_r, (nd & 0xfffcu) + eot_d, \
-                          (nk & 0xfffcu) + eot_k, tk_base);                                       \
-        }                                                                                         \
+        const uint32_t x = cc[J] + (pm & start2);                                                 \
+        ad[J] = (nd & ~pm & 0xfffcu) + (x & 0xffffu);                                             \
+        ak[J] = (nk & ~pm & 0xfffcu) + (x >> 16);                                                 \
+        nd = lds_u16(ad[J]);                                                                      \
+        nk = lds_u16(ak[J]);                                                                      \
+        pm = (uint32_t)((int32_t)(b16 << (31 - (H) - (J))) >> 31);                                \
+        m |= ((nd | nk) & ((pm & 2u) | 1u)) << (2 * (7 - (J)));                                   \
+    }
+
+#define SCAN_GROUP8(W, H, OFF)                                                                    \
+    {                                                                                             \
+        uint32_t cc[8], ad[8], ak[8], m = 0;                                                      \
+        SCAN_CLASSES8(W, H)                                                                       \
+        SCAN_STEP8(7, H) SCAN_STEP8(6, H) SCAN_STEP8(5, H) SCAN_STEP8(4, H)                       \
+        SCAN_STEP8(3, H) SCAN_STEP8(2, H) SCAN_STEP8(1, H) SCAN_STEP8(0, H)                       \
+        if (__builtin_expect(m != 0, 0))                                                          \
+            scan_emit8(ev, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
     }
 
 #define SCAN_SUB(W, OFF)                                                                          \
     {                                                                                             \
-        uint32_t cc[8];                                                                           \
         const uint32_t b16 = (uint32_t)(bits >> (OFF)) & 0xffffu;                                 \
-        SCAN_CLASSES8(W, 8)                                                                       \
-        SCAN_STEP8(7, 8, OFF) SCAN_STEP8(6, 8, OFF) SCAN_STEP8(5, 8, OFF) SCAN_STEP8(4, 8, OFF)   \
-        SCAN_STEP8(3, 8, OFF) SCAN_STEP8(2, 8, OFF) SCAN_STEP8(1, 8, OFF) SCAN_STEP8(0, 8, OFF)   \
-        SCAN_CLASSES8(W, 0)                                                                       \
-        SCAN_STEP8(7, 0, OFF) SCAN_STEP8(6, 0, OFF) SCAN_STEP8(5, 0, OFF) SCAN_STEP8(4, 0, OFF)   \
-        SCAN_STEP8(3, 0, OFF) SCAN_STEP8(2, 0, OFF) SCAN_STEP8(1, 0, OFF) SCAN_STEP8(0, 0, OFF)   \
+        SCAN_GROUP8(W, 8, OFF)                                                                    \
+        SCAN_GROUP8(W, 0, OFF)                                                                    \
     }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uint8_t* __restrict__ text,
@@ -311,30 +343,31 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
         const uint32_t len_r = hi_r - lo_r;
         const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
         const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
-        uint32_t sd = d_start, sk = k_start;
+        const uint32_t start2 = d_start | (k_start << 16);
+        uint32_t nd = 0, nk = 0, pm = 0xffffffffu;     // "previous byte started an utterance": start rows
         // aligned 64-byte blocks of the ADDRESS space, numbered from the one holding the batch base:
         // block bb covers relative positions [64 bb - r0, 64 bb - r0 + 64)
         const uintptr_t abase = (uintptr_t)(text + base);
         const uint32_t r0 = (uint32_t)(abase & 63);
-        const uint4* __restrict__ tpb = reinterpret_cast<const uint4*>(abase - r0);
+        const uintptr_t tpb = abase - r0;                           // global loads (see gload16)
         const uint32_t bb_hi = (hi_r + r0) >> 6, bb_lo = (lo_r + r0) >> 6;
         // the top block: only chunks holding a batch byte are read (the rest step as zero bytes
         // before the end-of-batch / next-utterance reset)
         const uint32_t q_end = (end_r - 1 + r0) >> 4;               // last chunk with a batch byte
-        uint4 n0 = tpb[4 * bb_hi], n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
-        if (4 * bb_hi + 1 <= q_end) n1 = tpb[4 * bb_hi + 1];
-        if (4 * bb_hi + 2 <= q_end) n2 = tpb[4 * bb_hi + 2];
-        if (4 * bb_hi + 3 <= q_end) n3 = tpb[4 * bb_hi + 3];
+        uint4 n0 = gload16(tpb + (uintptr_t)bb_hi * 64u), n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
+        if (4 * bb_hi + 1 <= q_end) n1 = gload16(tpb + (uintptr_t)bb_hi * 64u + 16);
+        if (4 * bb_hi + 2 <= q_end) n2 = gload16(tpb + (uintptr_t)bb_hi * 64u + 32);
+        if (4 * bb_hi + 3 <= q_end) n3 = gload16(tpb + (uintptr_t)bb_hi * 64u + 48);
         uint64_t nb = words[c];
         for (uint32_t bb = bb_hi;; --bb) {
             const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
             const uint64_t bits = nb;
             if (bb > bb_lo) {
-                const uint4* q = tpb + 4 * (bb - 1);
-                n0 = q[0];
-                n1 = q[1];
-                n2 = q[2];
-                n3 = q[3];
+                const uintptr_t q = tpb + (uintptr_t)(bb - 1) * 64u;
+                n0 = gload16(q);
+                n1 = gload16(q + 16);
+                n2 = gload16(q + 32);
+                n3 = gload16(q + 48);
                 const uint32_t i = bb_hi - (bb - 1);
                 nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * n_chunks + c]
                                               : block_bits_slow(offs, first_utt, c, i, (int64_t)((uintptr_t)text & 63));
@@ -350,6 +383,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
     lane_cnt[c] = cnt;
 }
 #undef SCAN_STEP8
+#undef SCAN_GROUP8
 #undef SCAN_CLASSES8
 #undef SCAN_SUB
 
