@@ -171,10 +171,86 @@ __device__ __attribute__((noinline)) uint64_t block_bits_slow(const uint64_t* __
     return bits;
 }
 
+// ------------------------------------------------------------------ lane order (k_scan balance)
+// A wavefront of k_scan runs as long as its longest lane (a lane is ~1 KiB of WHOLE utterances, so
+// lengths spread over ~0.5-2 KiB: in batch order a wavefront's lanes are only ~80% busy).  The scan
+// therefore takes its lanes in order of decreasing length: a counting sort on 32-byte length buckets
+// gives slot -> lane (lane_perm) and lane -> slot (lane_pos); k_lane_bits writes each lane's start
+// words at its slot, so the scan's word loads stay coalesced.  The order is not deterministic (block
+// reservations race) but only the thread mapping depends on it: every lane's events, counts and
+// arena are the same.
+constexpr int LANE_NB = 128;                       // length buckets: 0 = longest (>= 127*32 B)
+__device__ __forceinline__ uint32_t lane_bucket(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
+                                                uint32_t c) {
+    const uint64_t len = offs[first_utt[c + 1]] - offs[first_utt[c]];
+    return (uint32_t)(LANE_NB - 1) - (uint32_t)min<uint64_t>(len >> 5, LANE_NB - 1);
+}
+
+constexpr uint32_t LANE_SORT_CHUNK = 4096;         // lanes per workgroup (few global reservations)
+
+__global__ __launch_bounds__(256) void k_lane_count(const uint64_t* __restrict__ offs,
+                                                    const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+                                                    uint32_t* __restrict__ bucket_cnt) {
+    __shared__ uint32_t h[LANE_NB];
+    for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK, c1 = min(c0 + LANE_SORT_CHUNK, n_chunks);
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) atomicAdd(&h[lane_bucket(offs, first_utt, c)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
+        if (h[i]) atomicAdd(&bucket_cnt[i], h[i]);
+}
+
+// bucket_cnt[0..NB) = counts (k_lane_count), bucket_cnt[NB..2NB) = reservation cursors (zeroed)
+__global__ __launch_bounds__(256) void k_lane_place(const uint64_t* __restrict__ offs,
+                                                    const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+                                                    uint32_t* __restrict__ bucket_cnt, uint32_t* __restrict__ lane_perm,
+                                                    uint32_t* __restrict__ lane_pos) {
+    constexpr int PER = LANE_SORT_CHUNK / 256;
+    __shared__ uint32_t base[LANE_NB], h[LANE_NB];
+    if (threadIdx.x < 64) {                        // exclusive prefix of the counts, one wavefront
+        uint32_t run = 0;
+        for (int k = 0; k < LANE_NB; k += 64) {
+            const uint32_t v = bucket_cnt[k + threadIdx.x];
+            uint32_t incl = v;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d);
+                if ((int)threadIdx.x >= d) incl += o;
+            }
+            base[k + threadIdx.x] = run + incl - v;
+            run += __shfl(incl, 63);
+        }
+    }
+    for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK;
+    uint32_t bk[PER], rk[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t c = c0 + j * 256 + threadIdx.x;
+        bk[j] = c < n_chunks ? lane_bucket(offs, first_utt, c) : 0u;
+        rk[j] = c < n_chunks ? atomicAdd(&h[bk[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
+        if (h[i]) base[i] += atomicAdd(&bucket_cnt[LANE_NB + i], h[i]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t c = c0 + j * 256 + threadIdx.x;
+        if (c < n_chunks) {
+            const uint32_t t = base[bk[j]] + rk[j];
+            lane_perm[t] = c;
+            lane_pos[c] = t;
+        }
+    }
+}
+
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
 __global__ __launch_bounds__(256) void k_lane_bits(const uint64_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                   int64_t mis, uint64_t* __restrict__ words) {
+                                                   int64_t mis, const uint32_t* __restrict__ lane_pos,
+                                                   uint64_t* __restrict__ words) {
     __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -194,6 +270,7 @@ __global__ __launch_bounds__(256) void k_lane_bits(const uint64_t* __restrict__ 
     if (hi < lo) return;
     const int64_t b_hi = (hi + mis) >> 6, b_lo = (lo + mis) >> 6;
     const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
+    const uint32_t slot = lane_pos[c];
     int64_t u = u1;
     int64_t su = uoff(u);
     for (int64_t i = 0; i < nw; ++i) {
@@ -208,7 +285,7 @@ __global__ __launch_bounds__(256) void k_lane_bits(const uint64_t* __restrict__ 
             --u;
             if (u >= (int64_t)u0) su = uoff(u);
         }
-        words[(uint64_t)i * n_chunks + c] = bits;
+        words[(uint64_t)i * n_chunks + slot] = bits;
     }
 }
 
@@ -312,7 +389,8 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ offs, uint32_t n_utt,
                                                      const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                     const uint64_t* __restrict__ words, Event* __restrict__ ev,
+                                                     const uint64_t* __restrict__ words,
+                                                     const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
@@ -329,8 +407,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
         for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
     }
     __syncthreads();
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
+    if (t >= n_chunks) return;
+    const uint32_t c = lane_perm[t];
     const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
     const uint64_t base = offs[0];
     // positions relative to the batch base fit 32 bits (PII_MAX_BATCH_BYTES); 32-bit arithmetic keeps
@@ -358,7 +437,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
         if (4 * bb_hi + 1 <= q_end) n1 = gload16(tpb + (uintptr_t)bb_hi * 64u + 16);
         if (4 * bb_hi + 2 <= q_end) n2 = gload16(tpb + (uintptr_t)bb_hi * 64u + 32);
         if (4 * bb_hi + 3 <= q_end) n3 = gload16(tpb + (uintptr_t)bb_hi * 64u + 48);
-        uint64_t nb = words[c];
+        uint64_t nb = words[t];
         for (uint32_t bb = bb_hi;; --bb) {
             const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
             const uint64_t bits = nb;
@@ -369,7 +448,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
                 n2 = gload16(q + 32);
                 n3 = gload16(q + 48);
                 const uint32_t i = bb_hi - (bb - 1);
-                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * n_chunks + c]
+                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * n_chunks + t]
                                               : block_bits_slow(offs, first_utt, c, i, (int64_t)((uintptr_t)text & 63));
             }
             const uint32_t bpos = 64u * bb - r0;        // relative position of the block's byte 0 (mod 2^32)
@@ -2416,6 +2495,9 @@ struct pii_engine {
     pii_span* fd = nullptr;
     uint32_t *n_ev = nullptr, *n_find = nullptr, *out_len = nullptr, *incl = nullptr, *agg_f = nullptr;
     uint32_t* first_utt = nullptr;
+    uint32_t* lane_perm = nullptr;     // k_scan slot -> lane (longest lanes first)
+    uint32_t* lane_pos = nullptr;      // lane -> slot
+    uint32_t* lane_bkt = nullptr;      // [2 * LANE_NB] bucket counts + reservation cursors
     uint32_t* lane_cnt = nullptr;
     uint64_t* bnd = nullptr;
     EvLoc* evloc = nullptr;
@@ -2536,6 +2618,9 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
     if (n_lanes + 2 > e->cap_lanes) {
         const uint64_t nl = std::max<uint64_t>(n_lanes + n_lanes / 8 + 2, 1024);
         if ((rc = grow(e, e->first_utt, nl))) return rc;
+        if ((rc = grow(e, e->lane_perm, nl))) return rc;
+        if ((rc = grow(e, e->lane_pos, nl))) return rc;
+        if ((rc = grow(e, e->lane_bkt, 2 * LANE_NB))) return rc;
         if ((rc = grow(e, e->lane_cnt, nl))) return rc;
         if ((rc = grow(e, e->lane_ev, nl))) return rc;
         if ((rc = grow(e, e->bnd, nl * LANE_WORDS))) return rc;
@@ -2641,11 +2726,16 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                                 e->first_utt, e->out_len, e->n_find, e->kw,
                                                                 win_ctx ? e->wc_n : nullptr);
         if (n_chunks > 0) {
+            HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
+            const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
+            k_lane_count<<<nsb, 256, 0, st>>>(offs, e->first_utt, n_chunks, e->lane_bkt);
+            k_lane_place<<<nsb, 256, 0, st>>>(offs, e->first_utt, n_chunks, e->lane_bkt,
+                                                                 e->lane_perm, e->lane_pos);
             k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(offs, e->first_utt, n_chunks,
-                                                                (int64_t)((uintptr_t)text & 63), e->bnd);
+                                                                (int64_t)((uintptr_t)text & 63), e->lane_pos, e->bnd);
             HIPCHK(hipEventRecord(e->kev[0], st));
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
-                R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->ev, e->lane_cnt);
+                R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->lane_perm, e->ev, e->lane_cnt);
             HIPCHK(hipEventRecord(e->kev[1], st));
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
             k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
@@ -3157,7 +3247,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,

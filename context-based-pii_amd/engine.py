@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpii.so")
+LIB_PATH = os.environ.get("PII_LIB") or os.path.join(HERE, "libpii.so")   # PII_LIB: kernel experiments
 
 PII_OK, PII_E_ARG, PII_E_RULES, PII_E_DEVICE, PII_E_CAPACITY, PII_E_ORDER, PII_E_NOMEM = 0, -1, -2, -3, -4, -5, -6
 ROLE_CUSTOMER, ROLE_AGENT, ROLE_OTHER = 0, 1, 2
