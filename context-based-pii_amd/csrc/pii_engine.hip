@@ -41,7 +41,10 @@ constexpr int SCAN_BLOCK = 512;
 constexpr int CTX_BLOCK = 1024;
 constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
-constexpr uint32_t BYTES_PER_LANE = 1024;    // largest scan lane (big batches)
+#ifndef BYTES_PER_LANE_N
+#define BYTES_PER_LANE_N 1024
+#endif
+constexpr uint32_t BYTES_PER_LANE = BYTES_PER_LANE_N;    // largest scan lane (big batches)
 constexpr uint32_t MIN_LANE_SHIFT = 7;        // smallest scan lane, 128 B (small batches need lanes, not bytes)
 constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
