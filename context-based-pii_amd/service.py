@@ -22,6 +22,15 @@ the realtime handler reads it) and lives beside the slot map; its expiry follows
 Throughput path: ``process_batch`` runs many rows in one engine call (the batch contract of
 include/pii_engine.h: a conversation's rows contiguous and in entry order).
 
+Stream formats: ``process_pubsub_batch`` takes the raw Pub/Sub utterance
+payloads (``{conversation_id, original_entry_index, participant_role, text, user_id,
+start_timestamp_usec}``, main_service/main.py:295-302) in any order, validates them as
+subscriber_service/main.py:172-190 does, redacts them in one engine call and returns the redacted
+payloads the subscriber publishes (subscriber_service/main.py:213-221, ``original_text`` kept).
+``TranscriptArchive`` keeps those per conversation and emits the aggregator's GCS object
+``{"entries": [...]}`` ordered by ``original_entry_index`` (transcript_aggregator_service/main.py:
+150-160, 220-247) directly, without the Firestore round trip.
+
 Aggregator path (transcript_aggregator_service, README.md:131-134, 159-168): ``rescan_window_batch``
 appends each row to its conversation's window of the last N utterances (N = 5,
 transcript_aggregator_service/cloudbuild.yaml:33) and returns the redacted "\\n"-joined window, the
@@ -260,3 +269,74 @@ class PiiService:
                 if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
                     self.agent_text[slots[i]] = (r["text"], ts[i])
             return [_dec(res.text(i)) for i in range(len(rows))]
+
+    # ---------------------------------------------------------------- Pub/Sub stream formats (§8(f))
+    REQUIRED_FIELDS = ("conversation_id", "original_entry_index", "participant_role", "text",
+                       "start_timestamp_usec")
+
+    def process_pubsub_batch(self, payloads: Sequence[dict]) -> List[dict]:
+        """Raw utterance payloads -> redacted payloads (subscriber_service/main.py:213-221), in input
+        order.  A payload missing a required field (subscriber_service/main.py:172-187, same field
+        list and emptiness test) or with an empty role yields {"error": "Bad Request", "status": 400}
+        in its place and is not sent to the engine.  Rows are grouped by conversation and ordered by
+        original_entry_index before the engine call (the batch contract), so agent context reaches
+        the later customer rows of the same batch exactly as the per-message handlers would."""
+        out: List[Optional[dict]] = [None] * len(payloads)
+        good = []
+        for i, m in enumerate(payloads):
+            missing = [f for f in self.REQUIRED_FIELDS
+                       if m.get(f) is None or (isinstance(m.get(f), str) and not m.get(f).strip())]
+            role = str(m.get("participant_role") or "").upper()
+            if missing or not role:
+                out[i] = {"error": "Bad Request", "status": 400, "missing_fields": missing}
+                continue
+            good.append(i)
+        first = {}
+        for i in good:
+            first.setdefault(payloads[i]["conversation_id"], len(first))
+        order = sorted(good, key=lambda i: (first[payloads[i]["conversation_id"]],
+                                            int(payloads[i]["original_entry_index"]), i))
+        rows = [dict(payloads[i], participant_role=str(payloads[i]["participant_role"]).upper()) for i in order]
+        red = self.process_batch(rows) if rows else []
+        for i, r, t in zip(order, rows, red):
+            out[i] = {"conversation_id": r["conversation_id"],
+                      "original_entry_index": r["original_entry_index"],
+                      "text": t,
+                      "original_text": r["text"],
+                      "participant_role": r["participant_role"],
+                      "user_id": r.get("user_id"),
+                      "start_timestamp_usec": r["start_timestamp_usec"]}
+        return out
+
+
+class TranscriptArchive:
+    """The aggregator's per-conversation store of redacted utterances (Firestore
+    conversations/{id}/utterances, transcript_aggregator_service/main.py:150-160) and its final
+    object {"entries": [...]} ordered by original_entry_index (main.py:220-247)."""
+
+    FIELDS = ("text", "original_entry_index", "participant_role", "user_id", "start_timestamp_usec")
+
+    def __init__(self):
+        self.conv: Dict[object, Dict[int, dict]] = {}
+
+    def add(self, redacted_payloads: Sequence[dict]) -> None:
+        for p in redacted_payloads:
+            if not p or "error" in p:
+                continue
+            e = {f: p.get(f) for f in self.FIELDS}
+            if p.get("original_text"):
+                e["original_text"] = p["original_text"]
+            self.conv.setdefault(p["conversation_id"], {})[int(p["original_entry_index"])] = e
+
+    def entries(self, conversation_id) -> dict:
+        utts = self.conv.get(conversation_id, {})
+        return {"entries": [utts[k] for k in sorted(utts)]}
+
+    def conversation_ended(self, conversation_id) -> Optional[str]:
+        """The GCS object body (json.dumps(..., indent=2), main.py:236) or None when the conversation
+        has no utterances (the reference skips the upload); the conversation is dropped."""
+        import json
+        utts = self.conv.pop(conversation_id, None)
+        if not utts:
+            return None
+        return json.dumps({"entries": [utts[k] for k in sorted(utts)]}, indent=2)

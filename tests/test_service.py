@@ -212,3 +212,56 @@ def test_service_window_rescan_on_gpu(oracle_cfg):
             assert got == exp, (mode, name)
             svc.conversation_ended(cid)
             assert svc.engine.window_count(svc.slots.peek(cid)) == 0
+
+
+def _pubsub_payloads(tr):
+    """The golden transcripts as raw Pub/Sub payloads (main_service/main.py:295-302), interleaved
+    across conversations and shuffled (seeded): the stream order the subscriber sees."""
+    import random
+    out = []
+    for name, t in tr.items():
+        for e in t["entries"]:
+            out.append({"conversation_id": "ps" + t["conversation_id"], "original_entry_index": e["i"],
+                        "participant_role": e["role"].lower(), "text": e["text"], "user_id": "u-" + name,
+                        "start_timestamp_usec": e["ts"]})
+    random.Random(20250718).shuffle(out)
+    return out
+
+
+def _check_pubsub(svc, oracle_cfg):
+    S = pkg("service")
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    pay = _pubsub_payloads(tr)
+    bad = [{"conversation_id": "x", "original_entry_index": 0, "participant_role": "AGENT", "text": "  ",
+            "start_timestamp_usec": 1}, {"conversation_id": "x", "text": "hi"}]
+    res = svc.process_pubsub_batch(pay + bad)
+    assert res[-2]["status"] == 400 and res[-2]["missing_fields"] == ["text"]
+    assert res[-1]["status"] == 400 and "original_entry_index" in res[-1]["missing_fields"]
+    archive = S.TranscriptArchive()
+    archive.add(res)
+    for name, t in tr.items():
+        cid = "ps" + t["conversation_id"]
+        want = _oracle_replay(oracle_cfg, sorted(t["entries"], key=lambda e: e["i"]), cid)
+        got = {p["original_entry_index"]: p for p in res if p.get("conversation_id") == cid}
+        for e, w in zip(sorted(t["entries"], key=lambda e: e["i"]), want):
+            p = got[e["i"]]
+            assert p["text"] == w and p["original_text"] == e["text"]
+            assert p["participant_role"] == e["role"].upper() and p["user_id"] == "u-" + name
+        body = archive.conversation_ended(cid)
+        ent = json.loads(body)["entries"]
+        assert [x["original_entry_index"] for x in ent] == sorted(e["i"] for e in t["entries"])
+        assert [x["text"] for x in ent] == want
+    assert archive.conversation_ended("nope") is None
+
+
+def test_pubsub_batch_and_archive(svc, oracle_cfg):
+    """§8(f) stream formats over the engine double: shuffled raw payloads in, redacted payloads
+    (subscriber_service/main.py:213-221) out in input order, bad payloads 400, and the aggregator's
+    {"entries": [...]} object (transcript_aggregator_service/main.py:220-247)."""
+    _check_pubsub(svc, oracle_cfg)
+
+
+@pytest.mark.gpu
+def test_pubsub_batch_and_archive_on_gpu(oracle_cfg):
+    S = pkg("service")
+    _check_pubsub(S.PiiService(n_slots=64, clock=Clock()), oracle_cfg)
