@@ -1051,115 +1051,141 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
             out_len[u] = (uint32_t)(L + delta);
         }
     };
-    for (uint32_t i0 = 0; i0 < np; i0 += 4) {
-        int32_t ee[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ee[j] = i0 + j < np ? el[i0 + j] : -1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (ee[j] < 0) continue;
-            const PairRes P = rl[i0 + j];
-            const EvLoc Lc = evloc[P.ev];
-            const int ps = (int)(Lc.s - Lc.ustart);
-            if (Lc.u != u) {
-                if (u != 0xffffffffu) {
-                    flush_start();
-                    flush_utt();
-                }
-                u = Lc.u;
-                v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
-                minlik = vmin[v];
-                L = (int)(Lc.uend - Lc.ustart);
-                fdu = fd + Lc.ustart / R.min_len;
-#pragma unroll
-                for (int q = 0; q < LIVE; ++q) {
-                    lp[q] = -1;
-                    le[q] = -1;
-                }
-                spilled = false;
-                ex_valid = 0;
-                max_end = 0;
-                nf = 0;
-                delta = 0;
-                s = ps;
-            } else if (ps != s) {
+    auto pair = [&](uint32_t i, int e) {
+        const PairRes P = rl[i];
+        const EvLoc Lc = evloc[P.ev];
+        const int ps = (int)(Lc.s - Lc.ustart);
+        if (Lc.u != u) {
+            if (u != 0xffffffffu) {
                 flush_start();
-                s = ps;
+                flush_utt();
             }
-            const int p = P.p;
-            const int t = dtype[p];
-            if (!ven[v * T + t]) continue;
-            int prev_end = -1;
-            if (spilled) {
-                prev_end = (int)cur_s[p];
-            } else {
+            u = Lc.u;
+            v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
+            minlik = vmin[v];
+            L = (int)(Lc.uend - Lc.ustart);
+            fdu = fd + Lc.ustart / R.min_len;
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q) {
+                lp[q] = -1;
+                le[q] = -1;
+            }
+            spilled = false;
+            ex_valid = 0;
+            max_end = 0;
+            nf = 0;
+            delta = 0;
+            s = ps;
+        } else if (ps != s) {
+            flush_start();
+            s = ps;
+        }
+        const int p = P.p;
+        const int t = dtype[p];
+        if (!ven[v * T + t]) return;
+        int prev_end = -1;
+        if (spilled) {
+            prev_end = (int)cur_s[p];
+        } else {
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q)
+                if (lp[q] == p) prev_end = le[q];
+        }
+        if (s < prev_end) return;               // inside p's previous match (finditer)
+        if (spilled) {
+            cur_s[p] = (uint32_t)e;
+        } else {
+            int slot = -1;
+#pragma unroll
+            for (int q = 0; q < LIVE; ++q)
+                if (lp[q] == p) slot = q;
+            if (slot < 0) {
 #pragma unroll
                 for (int q = 0; q < LIVE; ++q)
-                    if (lp[q] == p) prev_end = le[q];
+                    if (slot < 0 && le[q] <= s) slot = q;
             }
-            if (s < prev_end) continue;               // inside p's previous match (finditer)
-            const int e = ee[j];
-            if (spilled) {
-                cur_s[p] = (uint32_t)e;
-            } else {
-                int slot = -1;
+            if (slot >= 0) {
 #pragma unroll
                 for (int q = 0; q < LIVE; ++q)
-                    if (lp[q] == p) slot = q;
-                if (slot < 0) {
-#pragma unroll
-                    for (int q = 0; q < LIVE; ++q)
-                        if (slot < 0 && le[q] <= s) slot = q;
-                }
-                if (slot >= 0) {
-#pragma unroll
-                    for (int q = 0; q < LIVE; ++q)
-                        if (q == slot) {
-                            lp[q] = p;
-                            le[q] = e;
-                        }
-                } else {
-                    for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
-#pragma unroll
-                    for (int q = 0; q < LIVE; ++q)
-                        if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
-                    cur_s[p] = (uint32_t)e;
-                    spilled = true;
-                }
-            }
-            const int xi = dex[p];
-            const int lik = P.lik;
-            if (lik < minlik) {                        // invalid (-1) or below min_likelihood
-                if (xi != 0xff) ex_valid &= ~(1u << xi);
-                continue;
-            }
-            if (xi != 0xff) {
-#pragma unroll
-                for (int x = 0; x < NE_MAX; ++x)
-                    if (x == xi) {
-                        ex_s[x] = s;
-                        ex_e[x] = e;
-                        ex_t[x] = t;
+                    if (q == slot) {
+                        lp[q] = p;
+                        le[q] = e;
                     }
-                ex_valid |= 1u << xi;
-            }
-            const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
-            bool excluded = false;
-            for (uint32_t q = x0; q < x1; ++q) {
-                const int xt = xids[q];
+            } else {
+                for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
 #pragma unroll
-                for (int x = 0; x < NE_MAX; ++x)
-                    if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
-                        excluded = true;
+                for (int q = 0; q < LIVE; ++q)
+                    if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
+                cur_s[p] = (uint32_t)e;
+                spilled = true;
             }
-            if (excluded) continue;
-            const bool better = best_e < 0 || e > best_e ||
-                                (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
-            if (better) {
-                best_e = e;
-                best_t = t;
-                best_lik = lik;
-            }
+        }
+        const int xi = dex[p];
+        const int lik = P.lik;
+        if (lik < minlik) {                        // invalid (-1) or below min_likelihood
+            if (xi != 0xff) ex_valid &= ~(1u << xi);
+            return;
+        }
+        if (xi != 0xff) {
+#pragma unroll
+            for (int x = 0; x < NE_MAX; ++x)
+                if (x == xi) {
+                    ex_s[x] = s;
+                    ex_e[x] = e;
+                    ex_t[x] = t;
+                }
+            ex_valid |= 1u << xi;
+        }
+        const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
+        bool excluded = false;
+        for (uint32_t q = x0; q < x1; ++q) {
+            const int xt = xids[q];
+#pragma unroll
+            for (int x = 0; x < NE_MAX; ++x)
+                if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
+                    excluded = true;
+        }
+        if (excluded) return;
+        const bool better = best_e < 0 || e > best_e ||
+                            (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
+        if (better) {
+            best_e = e;
+            best_t = t;
+            best_lik = lik;
+        }
+    };
+    // pend[] (4 B per pair, the lane's run at pend + lane_pair[c]) is read 16 entries per iteration as
+    // four aligned 16-byte loads, the next group issued before this one is decoded; only matched pairs
+    // (e >= 0, a small fraction) enter the body.  pend is allocated 16 entries past pair_cap, so the
+    // aligned groups never leave the allocation; entries outside the lane's run are masked off.
+    const uint64_t pbase = lane_pair[c];
+    const uint32_t off0 = (uint32_t)(pbase & 3u);
+    const int4* pa = reinterpret_cast<const int4*>(pend + (pbase - off0));
+    const uint32_t ng = (off0 + np + 15u) >> 4;
+    int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
+    for (uint32_t g = 0; g < ng; ++g) {
+        const int4 c0 = q0, c1 = q1, c2 = q2, c3 = q3;
+        if (g + 1 < ng) {
+            const int4* pn = pa + 4 * (g + 1);
+            q0 = pn[0];
+            q1 = pn[1];
+            q2 = pn[2];
+            q3 = pn[3];
+        }
+        const int32_t ev16[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                  c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m |= (uint32_t)(ev16[j] >= 0) << j;
+        // the lane's run is [off0, off0 + np) of the aligned groups
+        const uint32_t g0 = 16u * g;
+        if (g0 < off0) m &= 0xffffu << off0;
+        if (g0 + 16u > off0 + np) m &= (1u << (off0 + np - g0)) - 1u;
+        while (m) {
+            const uint32_t j = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t i = g0 + j - off0;
+            pair(i, el[i]);        // (the entry is in L1: its group was just loaded)
         }
     }
     if (u != 0xffffffffu) {
@@ -2603,7 +2629,7 @@ int grow_pairs(pii_engine* e, uint64_t cap) {
         return PII_E_NOMEM;
     }
     int rc;
-    if ((rc = grow(e, e->pres, cap)) || (rc = grow(e, e->pend, cap)) || (rc = grow(e, e->matched, cap)) ||
+    if ((rc = grow(e, e->pres, cap)) || (rc = grow(e, e->pend, cap + 16)) || (rc = grow(e, e->matched, cap)) ||
         (rc = grow(e, e->cont, cap)))
         return rc;
     return PII_OK;
