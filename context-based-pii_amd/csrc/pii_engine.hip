@@ -983,6 +983,20 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
 
 constexpr int LIVE = 8;            // register-resident "previous match end" slots per lane
 
+// bit j: entry g0 + j of an aligned 16-entry pend[] group is a match (>= 0) inside the lane's run
+// [off0, off0 + np)
+__device__ __forceinline__ uint32_t matched_mask16(int4 c0, int4 c1, int4 c2, int4 c3, uint32_t g0,
+                                                   uint32_t off0, uint32_t np) {
+    const int32_t v[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                           c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m |= (uint32_t)(v[j] >= 0) << j;
+    if (g0 < off0) m &= 0xffffu << off0;
+    if (g0 + 16u > off0 + np) m &= (1u << (off0 + np - g0)) - 1u;
+    return m;
+}
+
 // Per scan lane: its pairs in (utterance, start, accept-set) order.  Unmatched pairs change no state
 // (finditer skipping, exclusion and overlap only see matches), so only matched ones are decoded.
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
@@ -1172,15 +1186,8 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
             q2 = pn[2];
             q3 = pn[3];
         }
-        const int32_t ev16[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                                  c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        uint32_t m = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) m |= (uint32_t)(ev16[j] >= 0) << j;
-        // the lane's run is [off0, off0 + np) of the aligned groups
         const uint32_t g0 = 16u * g;
-        if (g0 < off0) m &= 0xffffu << off0;
-        if (g0 + 16u > off0 + np) m &= (1u << (off0 + np - g0)) - 1u;
+        uint32_t m = matched_mask16(c0, c1, c2, c3, g0, off0, np);
         while (m) {
             const uint32_t j = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -1896,9 +1903,7 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         lp[q] = -1;
         le[q] = -1;
     }
-    for (uint32_t i = 0; i < np; ++i) {
-        const int e = pend[base + i];
-        if (e < 0) continue;
+    auto cand = [&](uint32_t i, int e) {
         const PairRes P = pres[base + i];
         const EvLoc Lc = evloc[P.ev];
         const int s = (int)(Lc.s - Lc.ustart);
@@ -1925,7 +1930,7 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
             for (int q = 0; q < LIVE; ++q)
                 if (lp[q] == p) prev_end = le[q];
         }
-        if (s < prev_end) continue;                    // inside p's previous match (finditer)
+        if (s < prev_end) return;                    // inside p's previous match (finditer)
         if (spilled) {
             cur_s[p] = (uint32_t)e;
         } else {
@@ -1954,7 +1959,7 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
                 spilled = true;
             }
         }
-        if (P.lik < 0) continue;                       // validator failed
+        if (P.lik < 0) return;                       // validator failed
         WCand C;
         C.s = (uint32_t)s;
         C.e = (uint32_t)e;
@@ -1964,6 +1969,29 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         C.hotx = C.hot;
         C.pad = 0;
         wc[base + k++] = C;
+    };
+    // the lane's pend[] run in prefetched 16-entry groups, matched pairs only (as in k_select)
+    const uint32_t off0 = (uint32_t)(base & 3u);
+    const int4* pa = reinterpret_cast<const int4*>(pend + (base - off0));
+    const uint32_t ng = (off0 + np + 15u) >> 4;
+    int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
+    for (uint32_t g = 0; g < ng; ++g) {
+        const int4 c0 = q0, c1 = q1, c2 = q2, c3 = q3;
+        if (g + 1 < ng) {
+            const int4* pn = pa + 4 * (g + 1);
+            q0 = pn[0];
+            q1 = pn[1];
+            q2 = pn[2];
+            q3 = pn[3];
+        }
+        const uint32_t g0 = 16u * g;
+        uint32_t m = matched_mask16(c0, c1, c2, c3, g0, off0, np);
+        while (m) {
+            const uint32_t j = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t i = g0 + j - off0;
+            cand(i, pend[base + i]);
+        }
     }
     if (u != 0xffffffffu && k > uf) {
         wc_first[u] = (uint32_t)(base + uf);
