@@ -720,8 +720,10 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const u
         int64_t s_u = cnt ? uoff(u) : 0;
         bool agent = cnt ? uagent(u) : false;
         int g = KW_NONE;
+        Event En = cnt ? evl[0] : Event{};
         for (uint32_t k = 0; k < cnt; ++k) {
-            const Event E = evl[k];
+            const Event E = En;
+            if (k + 1 < cnt) En = evl[k + 1];      // next event in flight while this one decodes
             const int64_t pos = E.pos;
             while (pos < s_u) {
                 if (g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
@@ -755,8 +757,10 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const u
     int64_t u = u_top;
     int64_t s_u = uoff(u);
     int64_t e_u = uoff(u + 1);
+    Event En = evl[0];
     for (uint32_t k = 0; k < cnt; ++k) {
-        const Event E = evl[k];
+        const Event E = En;
+        if (k + 1 < cnt) En = evl[k + 1];
         const int64_t pos = E.pos;
         while (pos < s_u) {
             --u;
