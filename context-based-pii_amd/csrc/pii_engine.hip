@@ -800,16 +800,42 @@ __global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs*
     }
     __syncthreads();
     const uint64_t n = *ev_count;
-    for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
-        const EvPairs ep = evpairs[k];
-        if (ep.n == 0) continue;
-        const uint32_t a0 = small ? s_off[ep.acc] : R.d_acc_off[ep.acc];
-        for (uint32_t i = 0; i < ep.n; ++i) {
-            PairRes P;
-            P.ev = (uint32_t)k;
-            P.p = small ? s_ids[a0 + i] : R.d_acc_ids[a0 + i];
-            P.lik = -1;
-            pres[ep.first + i] = P;
+    // wave-cooperative: the pairs of the wavefront's 64 events are numbered 0..total-1 by an inclusive
+    // scan of the counts, and lane f writes pair f, f + 64, ... (its event found by a 6-step search of
+    // the scan), so a store instruction writes 64 neighbouring records instead of record i of 64 events
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t kb = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); kb < n; kb += stride) {
+        const uint64_t k = kb + lane;
+        EvPairs ep{0, 0, 0};
+        if (k < n) ep = evpairs[k];
+        const uint32_t a0 = ep.n == 0 ? 0u : (small ? s_off[ep.acc] : R.d_acc_off[ep.acc]);
+        uint32_t incl = ep.n;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+            const uint32_t f = f0 + lane;
+            // owner: the first lane whose inclusive count exceeds f
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const uint32_t v = __shfl(incl, lo + step - 1);
+                if (v <= f) lo += step;
+            }
+            const uint32_t o_incl = __shfl(incl, lo), o_n = __shfl((uint32_t)ep.n, lo);
+            const uint32_t o_a0 = __shfl(a0, lo), o_first = __shfl(ep.first, lo);
+            if (f < total) {
+                const uint32_t i = f - (o_incl - o_n);
+                PairRes P;
+                P.ev = (uint32_t)(kb + lo);
+                P.p = small ? s_ids[o_a0 + i] : R.d_acc_ids[o_a0 + i];
+                P.lik = -1;
+                pres[o_first + i] = P;
+            }
         }
     }
 }
