@@ -30,6 +30,7 @@ compiler = importlib.import_module("context-based-pii_amd.compiler")
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy ceiling
 LANE_BYTES = 1024        # BYTES_PER_LANE of csrc/pii_engine.hip (k_scan lane = utterances starting in 1 KiB)
 SOURCES = ["context-based-pii_amd/csrc/pii_engine.hip", "context-based-pii_amd/csrc/pii_device.h"]
+CFG2_MEAN_LEN = 120.8    # bytes per utterance of the config-2 corpus (1.208 GB / 10M)
 METRIC = "transcript MB/s scanned+redacted per node (1/2/4/8 GPU) and % HBM roofline"
 
 # --------------------------------------------------------------------------- CPU baseline (oracle)
@@ -51,30 +52,57 @@ def _cpu_work(rng):
     return time.perf_counter() - t0, int(o[hi] - o[lo])
 
 
-def cpu_baseline(bank, seconds: float = 15.0):
-    """The oracle (Python re + validators), multi-process over whole conversations on the host.
-    Calibrated on one 10-conversation block, then sized to about `seconds` of wall time."""
-    cores = min(16, os.cpu_count() or 1)
-    probe = synth.corpus_meta(10, 100, bank, seed=synth.SEED + 7)
-    pdata = synth.gather_bytes(probe, bank)
-    _cpu_init(pdata, probe.offsets.astype(np.int64), probe.role, probe.conv_slot, probe.ts_us)
-    dt, nb = _cpu_work((0, probe.n))
-    conv_rate = 10 / max(dt, 1e-6)                       # conversations / s / core
-    n_conv = int(min(30000, max(cores * 4, conv_rate * cores * seconds * 0.5)))   # probe is optimistic ~2x
+def cpu_share() -> int:
+    """Host cores this process may use: the cgroup CPU quota (the GPU box gives each GPU a share of
+    the host), else OMP_NUM_THREADS as the box sets it, else the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(n, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return min(n, int(env))
+    return n
+
+
+def host_cpu_model() -> str:
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(bank, min_bytes: float = 1e9):
+    """The oracle (Python re + validators), multi-process over whole conversations on this host's CPU
+    share, timed over at least `min_bytes` of the same synthetic distribution (SURVEY §8(d) /
+    BASELINE.md §2: the full 1.2 GB config would take minutes, so >= 1 GB is timed and reported as a
+    rate)."""
+    cores = cpu_share()
+    n_conv = int(min_bytes / (100 * CFG2_MEAN_LEN)) + 1
     meta = synth.corpus_meta(n_conv, 100, bank, seed=synth.SEED + 7)
     data = synth.gather_bytes(meta, bank)
     offs = meta.offsets.astype(np.int64)
-    chunks = [(i * 100, (i + 1) * 100) for i in range(n_conv)]
+    blocks = [(c * 100, min(c + 50, n_conv) * 100) for c in range(0, n_conv, 50)]   # 50 conversations each
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(cores, initializer=_cpu_init, initargs=(data, offs, meta.role, meta.conv_slot, meta.ts_us)) as pool:
-        res = pool.map(_cpu_work, chunks, chunksize=max(1, len(chunks) // (cores * 8)))
+        res = pool.map(_cpu_work, blocks, chunksize=1)
     wall = time.perf_counter() - t0
     nbytes = sum(b for _, b in res)
     return {"value": round(nbytes / wall / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
-            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e6:.1f} MB) of the same synthetic "
-                      f"distribution, oracle/pii_oracle.py process_rows, multiprocessing fork pool of {cores}, "
-                      f"wall {wall:.1f}s"}
+            "host_cpu": host_cpu_model(), "host_logical_cpus": os.cpu_count(),
+            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e9:.3f} GB) of the config-2 synthetic "
+                      f"distribution, oracle/pii_oracle.py process_rows over whole conversations, multiprocessing "
+                      f"fork pool of {cores} (this host's CPU share), wall {wall:.1f}s; the 1.208 GB config-2 batch "
+                      f"extrapolates to {1.208e9 / (nbytes / wall):.1f}s"}
 
 
 def source_digest() -> str:
@@ -122,71 +150,65 @@ def gpu_corpus(meta, bank, dev):
     return text, offs
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--conversations", type=int, default=100_000, help="per GPU")
-    ap.add_argument("--utt-per-conv", type=int, default=100)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window"], default="scan",
-                    help="scan = config 2 (headline); window = config 3 multi-turn re-scan")
-    ap.add_argument("--window-n", type=int, default=5)
-    args = ap.parse_args()
-    if args.workload == "window":
-        return window_main(args)
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    bank = synth.build_bank(16384, 16384, seed=synth.SEED)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(bank, args.cpu_seconds)          # before any HIP initialisation (fork pool)
-
+def _sync(dev):
     import torch
-    import torch.distributed as dist
-    eng_mod = importlib.import_module("context-based-pii_amd.engine")
-    if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
-    # this rank's shard: conversations [rank*C, (rank+1)*C) -- the conversation-id sharding of
-    # SURVEY §8(e) (gpu = conversation_id % G on a dense id space)
+
+class DeviceBatch:
+    """One rank's resident config-2 shard: conversations [conv_base, conv_base + C) of the synthetic
+    corpus (gpu = conversation_id % G on a dense id space is a contiguous block here),
+    staged into device memory once, plus the output buffers."""
+
+    def __init__(self, C, U, bank, conv_base, dev):
+        import torch
+        self.meta = synth.corpus_meta(C, U, bank, seed=synth.SEED, conv_base=conv_base)
+        self.text, self.offs = gpu_corpus(self.meta, bank, dev)
+        self.n = self.meta.n
+        self.n_bytes = int(self.meta.offsets[-1])
+        self.slot = torch.from_numpy((self.meta.conv_slot - conv_base).view(np.int32)).to(dev)
+        self.role = torch.from_numpy(self.meta.role).to(dev)
+        self.ts = torch.from_numpy(self.meta.ts_us).to(dev)
+        self.out_cap = self.n_bytes + 48 * self.n
+        self.span_cap = self.n * 2
+        self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
+        self.out_offs = torch.empty(self.n + 1, dtype=torch.int64, device=dev)
+        self.spans = torch.empty(self.span_cap * 16, dtype=torch.uint8, device=dev)
+        self.ctx = torch.empty(self.n, dtype=torch.int16, device=dev)
+
+    def run(self, eng):
+        eng.scan_redact_device(self.text.data_ptr(), self.offs.data_ptr(), self.n, self.slot.data_ptr(),
+                               self.role.data_ptr(), self.ts.data_ptr(), self.out.data_ptr(), self.out_cap,
+                               self.out_offs.data_ptr(), self.spans.data_ptr(), self.span_cap, self.ctx.data_ptr())
+
+
+def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None):
+    """One rank of the config-2 benchmark: shard -> W warmup steps -> K timed steps between barriers
+    + device syncs -> max-over-ranks time.  A step = one scan+redact pass over the rank's resident
+    shard + the all-reduce of the u64[T+1] per-infoType histogram (the only collective; reset every
+    step).  After timing, the reduced histogram of the last step is checked against an all-gather
+    of every rank's own counts.  Returns the JSON line on rank 0 (None elsewhere)."""
+    import torch
+    bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
     C, U = args.conversations, args.utt_per_conv
-    meta = synth.corpus_meta(C, U, bank, seed=synth.SEED, conv_base=rank * C)
-    text, offs = gpu_corpus(meta, bank, dev)
-    n = meta.n
-    n_bytes = int(meta.offsets[-1])
-    slot = torch.from_numpy((meta.conv_slot - rank * C).view(np.int32)).to(dev)
-    role = torch.from_numpy(meta.role).to(dev)
-    ts = torch.from_numpy(meta.ts_us).to(dev)
-    out_cap = n_bytes + 48 * n
-    span_cap = n * 2
-    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
-    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
-    d_ctx = torch.empty(n, dtype=torch.int16, device=dev)
-    comp = compiler.compile_default()
-    eng = eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
+    B = DeviceBatch(C, U, bank, rank * C, dev)
+    eng = make_engine(B, bank, C)
     T = len(eng.type_names)
     hist = torch.zeros(T + 1, dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
+    local = np.zeros(T + 1, dtype=np.int64)
+    _sync(dev)
 
     def step():
-        eng.scan_redact_device(text.data_ptr(), offs.data_ptr(), n, slot.data_ptr(), role.data_ptr(),
-                               ts.data_ptr(), d_out.data_ptr(), out_cap, d_oo.data_ptr(), d_sp.data_ptr(),
-                               span_cap, d_ctx.data_ptr())
+        eng.histogram_reset()
+        B.run(eng)
         ob, ns, fl = eng.sync()
         if fl:
             raise RuntimeError(f"engine error flags {fl}")
+        local[:T] = eng.histogram().astype(np.int64)
+        local[T] = ns
         if world > 1:
-            h = torch.from_numpy(eng.histogram().astype(np.int64)).to(dev)
-            hist[:T] = h
-            hist[T] = ns
+            hist.copy_(torch.from_numpy(local))
             dist.all_reduce(hist)                           # RCCL over xGMI: per-infoType counts
         return ob, ns
 
@@ -194,7 +216,7 @@ def main():
         step()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     per_stage = np.zeros(6)
     k_ms = {"k_scan": 0.0, "k_redact": 0.0}
     t0 = time.perf_counter()
@@ -205,58 +227,130 @@ def main():
             k_ms[k] += v
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     elapsed = time.perf_counter() - t0
+    reduced = local.copy()
+    verified = bool(local[T] == local[:T].sum())
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        reduced = hist.cpu().numpy()
+        parts = [torch.zeros(T + 1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(local).to(dev))
+        want = np.sum([p.cpu().numpy() for p in parts], axis=0)
+        verified = bool((want == reduced).all() and reduced[T] == reduced[:T].sum())
     per_stage /= args.steps
     k_ms = {k: v / args.steps for k, v in k_ms.items()}
     n_pairs, n_events = eng.queue_sizes()
+    names = list(eng.type_names)
+    eng.close()
+    if rank != 0:
+        return None
+    n, n_bytes = B.n, B.n_bytes
     n_lanes = (n_bytes + LANE_BYTES - 1) // LANE_BYTES
     ms_step = elapsed / args.steps * 1e3
     total_bytes = n_bytes * world * args.steps
     mbps = total_bytes / elapsed / 1e6
     # SURVEY 8(d) whole-path algorithmic bytes: in + out + in/out offsets + slot/role + spans
-    B = n_bytes + ob + 8 * (n + 1) * 2 + 5 * n + 16 * ns
-    t_pipe = per_stage[5] / 1e3
+    Bw = n_bytes + ob + 8 * (n + 1) * 2 + 5 * n + 16 * ns
+    t_pipe = max(per_stage[5], 1e-9) / 1e3
     # dominant kernel k_scan, algorithmic bytes per launch (DESIGN.md "Roofline accounting"):
     # every utterance byte once + the utterance-start bitmap (1 bit per byte) + per lane its
     # first_utt pair, offsets pair, event count (24 B) + 8 B per event written
     scan_B = n_bytes + (n_bytes + 63) // 64 * 8 + 24 * n_lanes + 8 * n_events
-    scan_GBps = scan_B / (k_ms["k_scan"] / 1e3) / 1e9
+    scan_GBps = scan_B / max(k_ms["k_scan"] / 1e3, 1e-12) / 1e9
     # k_redact: input + output bytes, its offset/count reads, the span copy (read + write)
     red_B = n_bytes + ob + 8 * (n + 1) * 3 + 4 * n + 32 * ns
-    red_GBps = red_B / (k_ms["k_redact"] / 1e3) / 1e9
+    red_GBps = red_B / max(k_ms["k_redact"] / 1e3, 1e-12) / 1e9
     traffic = measured_traffic("k_scan", n_bytes)
+    return {
+        "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "config2: per GPU 100k conversations x 100 utterances (10M utterances, "
+                               "~120 B lognormal) single-utterance scan+redact with expected_pii_type context",
+                   "utterances_per_gpu": n, "bytes_per_gpu": n_bytes, "parallelism": f"conversation-sharded x{world}",
+                   "rules": "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
+        "utt_per_s": round(n * world * args.steps / elapsed, 1),
+        "spans_per_step_per_gpu": int(ns),
+        "queues_per_step_per_gpu": {"scan_events": n_events, "candidate_pairs": n_pairs},
+        "stages_ms": {k: round(float(v), 4) for k, v in zip(
+            ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
+        "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
+        "pipeline": {"algorithmic_bytes": int(Bw), "GBps": round(Bw / t_pipe / 1e9, 1),
+                     "frac": round(Bw / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
+        "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "algorithmic_bytes": int(scan_B), "launch_ms": round(k_ms["k_scan"], 4)},
+        "roofline_redact": {"bound": "hbm", "kernel": "k_redact", "achieved": round(red_GBps, 1),
+                            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(red_GBps / HBM_PEAK_GBPS, 4),
+                            "algorithmic_bytes": int(red_B), "launch_ms": round(k_ms["k_redact"], 4)},
+        "histogram": {"collective": "all_reduce u64[T+1] (RCCL)" if world > 1 else "none (1 rank)",
+                      "total_spans_last_step": int(reduced[T]), "verified": verified,
+                      "per_type": {names[t]: int(reduced[t]) for t in range(T) if reduced[t]}},
+        "cpu_baseline": cpu,
+    }
+
+
+def _spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) without a launcher: start N rank processes with
+    torch.distributed.run from this GPU-free parent (no HIP call has happened here) and exit with
+    their status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--conversations", type=int, default=100_000, help="per GPU")
+    ap.add_argument("--utt-per-conv", type=int, default=100)
+    ap.add_argument("--bank", type=int, default=16384, help="agent / customer utterance bank size")
+    ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["scan", "window"], default="scan",
+                    help="scan = config 2 (headline); window = config 3 multi-turn re-scan")
+    ap.add_argument("--window-n", type=int, default=5)
+    args = ap.parse_args()
+    if args.workload == "window":
+        return window_main(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
+        cpu = cpu_baseline(bank, args.cpu_gb * 1e9)           # before any HIP initialisation (fork pool)
+
+    import torch
+    import torch.distributed as dist
+    eng_mod = importlib.import_module("context-based-pii_amd.engine")
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comp = compiler.compile_default()
+
+    def make_engine(batch, bank, C):
+        return eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
+    line = run_rank(args, rank, world, dev, make_engine, cpu=cpu, dist=dist if world > 1 else None)
     if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "config2: per GPU 100k conversations x 100 utterances (10M utterances, "
-                                   "~120 B lognormal) single-utterance scan+redact with expected_pii_type context",
-                       "utterances_per_gpu": n, "bytes_per_gpu": n_bytes, "parallelism": f"conversation-sharded x{world}",
-                       "rules": "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
-            "utt_per_s": round(n * world * args.steps / elapsed, 1),
-            "spans_per_step_per_gpu": ns,
-            "queues_per_step_per_gpu": {"scan_events": n_events, "candidate_pairs": n_pairs},
-            "stages_ms": {k: round(float(v), 4) for k, v in zip(
-                ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
-            "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
-            "pipeline": {"algorithmic_bytes": int(B), "GBps": round(B / t_pipe / 1e9, 1),
-                         "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
-            "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "algorithmic_bytes": int(scan_B), "launch_ms": round(k_ms["k_scan"], 4)},
-            "roofline_redact": {"bound": "hbm", "kernel": "k_redact", "achieved": round(red_GBps, 1),
-                                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(red_GBps / HBM_PEAK_GBPS, 4),
-                                "algorithmic_bytes": int(red_B), "launch_ms": round(k_ms["k_redact"], 4)},
-            "cpu_baseline": cpu,
-        }
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -277,7 +371,7 @@ def _cpu_window_work(rng):
 def cpu_window_baseline(bank, n_win: int, seconds: float = 15.0):
     """oracle.process_window_rows (full re-scan of every joined window: what the reference does per
     utterance) over whole conversations, multi-process on the host; MB/s of NEW utterance bytes."""
-    cores = min(16, os.cpu_count() or 1)
+    cores = cpu_share()
     probe = synth.corpus_meta(4, 100, bank, seed=synth.SEED + 7)
     pdata = synth.gather_bytes(probe, bank)
     _cpu_init(pdata, probe.offsets.astype(np.int64), probe.role, probe.conv_slot, probe.ts_us)

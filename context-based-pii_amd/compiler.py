@@ -52,6 +52,7 @@ VERY_LIKELY = 5
 DEFAULT_MIN_LIKELIHOOD = 3
 VALIDATOR_IDS = {None: 0, "luhn": 1, "nanp": 2, "ssn": 3, "ein": 4, "ipv4": 5, "swift": 6, "iban": 7}
 BLOB_MAGIC = b"PIIRULE1"
+PSEUDO_GROUP_MAX_TYPES = 64     # rule sets up to this many types get a context variant per type
 
 
 class RuleError(ValueError):
@@ -723,6 +724,14 @@ class Rules:
             usable = [k for k in kws if k and k == k.lower()]   # upper-case keywords never hit lower()ed text
             pat = "(?i)(?:" + "|".join(re.escape(k) for k in usable) + ")" if usable else None
             self.kw_groups.append((t, pat, always))
+        # Every other info type becomes a keyword-less context group, so that a context record naming
+        # it (call_dlp_for_redaction(transcript, {"expected_pii_type": t}), main.py:614-686) has a
+        # compiled variant.  extract_expected_pii never returns one (no keywords).  Large rule sets
+        # (config 5) skip this: V * T variant tables would not fit the kernels' LDS images.
+        self.n_keyword_groups = len(self.kw_groups)
+        if len(self.type_names) <= PSEUDO_GROUP_MAX_TYPES:
+            named = {t for t, _, _ in self.kw_groups}
+            self.kw_groups.extend((t, None, False) for t in self.type_names if t not in named)
 
     @classmethod
     def load(cls, dlp_config_path: Optional[str] = None, builtin_path: Optional[str] = None) -> "Rules":

@@ -20,7 +20,11 @@ transcript of the last keyword hit -- the record's ``agent_transcript`` field --
 the realtime handler reads it) and lives beside the slot map; its expiry follows the engine's TTL.
 
 Throughput path: ``process_batch`` runs many rows in one engine call (the batch contract of
-include/pii_engine.h: a conversation's rows contiguous and in entry order).
+include/pii_engine.h: a conversation's rows contiguous and in entry order), and
+``process_requests`` runs a micro-batch of concurrent handler requests in one engine call with the
+same results as calling the handlers one after another (``app.py`` is the Flask front end that
+coalesces concurrent HTTP requests into such micro-batches).  A batch with more conversations than
+the slot table holds is cut into runs that fit, so slot reuse never mixes two conversations.
 
 Stream formats: ``process_pubsub_batch`` takes the raw Pub/Sub utterance
 payloads (``{conversation_id, original_entry_index, participant_role, text, user_id,
@@ -75,20 +79,25 @@ def _dec(b: bytes) -> str:
 
 class SlotMap:
     """conversation_id -> engine context slot; slot 0 is reserved for stateless calls.  When all
-    slots are taken the least recently used conversation is evicted (its context is cleared)."""
+    slots are taken the least recently used conversation that is not pinned (part of the batch
+    being built) is evicted (its context is cleared)."""
 
     def __init__(self, n_slots: int, on_evict: Optional[Callable[[int], None]] = None):
-        if n_slots < 2:
-            raise ValueError("need at least 2 slots (slot 0 is reserved)")
+        if n_slots < 3:
+            raise ValueError("need at least 3 slots (slot 0 is reserved)")
         self.n_slots = n_slots
         self.on_evict = on_evict
         self._map: "OrderedDict[object, int]" = OrderedDict()
         self._free = list(range(n_slots - 1, 0, -1))
 
+    @property
+    def capacity(self) -> int:
+        return self.n_slots - 1
+
     def __len__(self):
         return len(self._map)
 
-    def get(self, conversation_id) -> int:
+    def get(self, conversation_id, pinned: Optional[set] = None) -> int:
         s = self._map.get(conversation_id)
         if s is not None:
             self._map.move_to_end(conversation_id)
@@ -96,7 +105,10 @@ class SlotMap:
         if self._free:
             s = self._free.pop()
         else:
-            _, s = self._map.popitem(last=False)
+            victim = next((c for c in self._map if not pinned or c not in pinned), None)
+            if victim is None:
+                raise RuntimeError("every slot is pinned by the current batch")
+            s = self._map.pop(victim)
             if self.on_evict:
                 self.on_evict(s)
         self._map[conversation_id] = s
@@ -105,19 +117,43 @@ class SlotMap:
     def peek(self, conversation_id) -> Optional[int]:
         return self._map.get(conversation_id)
 
+    def release(self, conversation_id) -> Optional[int]:
+        s = self._map.pop(conversation_id, None)
+        if s is not None:
+            self._free.append(s)
+        return s
+
+
+def role_code(participant_role) -> int:
+    """subscriber_service/main.py:189,200,229: AGENT -> agent handler, END_USER / CUSTOMER ->
+    customer handler; anything else is not a handler role."""
+    pr = str(participant_role or "").upper()
+    return ROLE_AGENT if pr == "AGENT" else ROLE_CUSTOMER if pr in ("END_USER", "CUSTOMER") else ROLE_OTHER
+
 
 class PiiService:
     """The main_service hot path on one engine (one GPU).  Thread-safe: calls serialize per engine,
-    like the reference's single DLP client shared by gunicorn threads."""
+    like the reference's single DLP client shared by gunicorn threads.
+
+    One time base per service (the context TTL compares two stamps of the same clock):
+    ``time_base="wall"`` (the reference: every record is stamped with time.time() when the handler
+    runs, main.py:370) stamps batch rows with the wall clock too; ``time_base="payload"`` (replays)
+    stamps rows with their ``start_timestamp_usec`` and makes the handlers' "now" the latest payload
+    time seen."""
 
     STATELESS_SLOT = 0
 
     def __init__(self, engine: Optional[Engine] = None, n_slots: int = 1 << 16,
-                 ttl_seconds: int = CONTEXT_TTL_SECONDS, clock: Callable[[], float] = time.time, device: int = 0):
+                 ttl_seconds: int = CONTEXT_TTL_SECONDS, clock: Callable[[], float] = time.time, device: int = 0,
+                 time_base: str = "wall"):
+        if time_base not in ("wall", "payload"):
+            raise ValueError("time_base must be 'wall' or 'payload'")
         self.engine = engine if engine is not None else Engine.from_rules(device=device, n_conv_slots=n_slots,
                                                                           ttl_seconds=ttl_seconds)
         self.ttl_us = int(ttl_seconds) * 1_000_000
         self.clock = clock
+        self.time_base = time_base
+        self._payload_now: Optional[int] = None
         self.lock = threading.Lock()
         self.slots = SlotMap(self.engine.n_slots, on_evict=self._evict)
         self.group_of_type: Dict[str, int] = {}
@@ -127,7 +163,16 @@ class PiiService:
 
     # ---------------------------------------------------------------- helpers
     def _now_us(self) -> int:
+        if self.time_base == "payload" and self._payload_now is not None:
+            return self._payload_now
         return int(self.clock() * 1_000_000)
+
+    def _row_ts(self, r: dict, now: int) -> int:
+        if self.time_base == "wall" or r.get("start_timestamp_usec") is None:
+            return now
+        t = int(r["start_timestamp_usec"])
+        self._payload_now = t if self._payload_now is None else max(self._payload_now, t)
+        return t
 
     def _evict(self, slot: int):
         self.engine.context_set(slot, -1, 0)
@@ -150,10 +195,28 @@ class PiiService:
     def _run(self, texts: Sequence[bytes], slots: Sequence[int], roles: Sequence[int], ts: Sequence[int]):
         return self.engine.scan_redact(texts, slots, roles, ts)
 
+    def _sub_batches(self, keys: Sequence[object], split_before: Optional[Sequence[bool]] = None) -> List[List[int]]:
+        """Row indices cut into runs whose distinct-conversation count fits the slot table (so
+        assigning slots for one run never evicts a conversation of the same run)."""
+        cap = self.slots.capacity - 1
+        out, cur, seen = [], [], set()
+        for i, k in enumerate(keys):
+            if cur and ((k not in seen and len(seen) >= cap) or (split_before and split_before[i])):
+                out.append(cur)
+                cur, seen = [], set()
+            cur.append(i)
+            seen.add(k)
+        if cur:
+            out.append(cur)
+        return out
+
     # ---------------------------------------------------------------- reference seam (main.py:580)
     def call_dlp_for_redaction(self, transcript: str, context: Optional[dict]) -> str:
         """Redact one transcript with an optional context record ({"expected_pii_type": ...}).
-        Stateless: the conversation table is not touched."""
+        Stateless: the conversation table is not touched.  Any expected_pii_type the engine has a
+        type for selects its compiled variant (main.py:614-686); a name the engine has no detector
+        for changes nothing the engine reports (the reference would add an info type and a rule set
+        for it, both of which only affect findings of that type)."""
         try:
             with self.lock:
                 now = self._now_us()
@@ -177,98 +240,174 @@ class PiiService:
 
     # ---------------------------------------------------------------- handlers (main.py:344-466)
     def handle_agent_utterance(self, data: Optional[dict]) -> Tuple[dict, int]:
-        if not data or "conversation_id" not in data or "transcript" not in data:
-            return {"error": "Missing conversation_id or transcript"}, 400
-        transcript = data["transcript"]
-        try:
-            with self.lock:
-                slot = self.slots.get(data["conversation_id"])
-                now = self._now_us()
-                res = self._run([_enc(transcript)], [slot], [ROLE_AGENT], [now])
-                g = int(res.ctx_info[0])
-                if g >= 0:
-                    self.agent_text[slot] = (transcript, now)
-                return {"redacted_transcript": _dec(res.text(0)), "context_stored": g >= 0}, 200
-        except PiiError as e:
-            return {"redacted_transcript": error_string(e.code, transcript), "context_stored": False}, 200
+        return self.process_requests([("agent", data)])[0]
 
     def handle_customer_utterance(self, data: Optional[dict]) -> Tuple[dict, int]:
-        if not data or "conversation_id" not in data or "transcript" not in data:
-            return {"error": "Missing conversation_id or transcript"}, 400
-        transcript = data["transcript"]
-        try:
-            with self.lock:
-                slot = self.slots.get(data["conversation_id"])
-                now = self._now_us()
-                used = self._context_record(slot, now) is not None
-                res = self._run([_enc(transcript)], [slot], [ROLE_CUSTOMER], [now])
-                return {"redacted_transcript": _dec(res.text(0)), "context_used": used}, 200
-        except PiiError as e:
-            return {"redacted_transcript": error_string(e.code, transcript), "context_used": False}, 200
+        return self.process_requests([("customer", data)])[0]
 
     def redact_utterance_realtime(self, data: Optional[dict]) -> Tuple[dict, int]:
-        if not data or "conversation_id" not in data or "utterance" not in data:
-            return {"error": "Missing conversation_id or utterance"}, 400
-        utterance = data["utterance"]
+        return self.process_requests([("realtime", data)])[0]
+
+    REQUEST_KEYS = {"agent": "transcript", "customer": "transcript", "realtime": "utterance"}
+
+    def process_requests(self, reqs: Sequence[Tuple[str, Optional[dict]]]) -> List[Tuple[dict, int]]:
+        """A micro-batch of handler requests [(kind, json body)] in arrival order, kind in
+        {"agent", "customer", "realtime"} (/handle-agent-utterance, /handle-customer-utterance,
+        /redact-utterance-realtime) -> [(response json, status)], in ONE engine call where possible.
+
+        Equivalent to calling the handlers one by one in arrival order: a conversation's requests
+        stay in arrival order (the engine's row order), conversations are independent.  A realtime
+        request reads the host-side agent transcript, which an AGENT row of its conversation earlier
+        in the same engine call would only update after the call, so such a request starts a new
+        engine call."""
+        out: List[Optional[Tuple[dict, int]]] = [None] * len(reqs)
+        valid = []
+        for i, (kind, data) in enumerate(reqs):
+            key = self.REQUEST_KEYS[kind]
+            if not data or "conversation_id" not in data or key not in data:
+                out[i] = ({"error": f"Missing conversation_id or {key}"}, 400)
+            else:
+                valid.append(i)
+        split, agents, cur_convs = [], set(), set()
+        cap = self.slots.capacity - 1
+        for i in valid:
+            kind, data = reqs[i]
+            cid = data["conversation_id"]
+            cut = (kind == "realtime" and cid in agents) or (cid not in cur_convs and len(cur_convs) >= cap)
+            if cut:
+                agents, cur_convs = set(), set()
+            split.append(cut)
+            cur_convs.add(cid)
+            if kind == "agent":
+                agents.add(cid)
+        for run in self._sub_batches([reqs[i][1]["conversation_id"] for i in valid], split):
+            self._run_requests(reqs, [valid[j] for j in run], out)
+        return out
+
+    def _run_requests(self, reqs, idxs: List[int], out) -> None:
         with self.lock:
-            slot = self.slots.peek(data["conversation_id"])
             now = self._now_us()
-            rec = self._context_record(slot, now) if slot is not None else None
-        if rec and "agent_transcript" in rec:
-            full = self.call_dlp_for_redaction(f"{rec['agent_transcript']}\n{utterance}", rec)
-            lines = full.splitlines()
-            redacted = lines[-1] if lines else ""
-        else:
-            redacted = self.call_dlp_for_redaction(utterance, rec)
-        return {"redacted_utterance": redacted}, 200
+            pinned = {reqs[i][1]["conversation_id"] for i in idxs}
+            rows = []                     # (slot, request index, text, role, realtime split)
+            for i in idxs:
+                kind, data = reqs[i]
+                cid = data["conversation_id"]
+                if kind == "realtime":
+                    slot = self.slots.peek(cid)
+                    rec = self._context_record(slot, now) if slot is not None else None
+                    utt = data["utterance"]
+                    if rec is None:                             # main.py:464 with no context
+                        rows.append((self.STATELESS_SLOT, i, utt, ROLE_OTHER, False))
+                    elif "agent_transcript" in rec:             # main.py:457-461
+                        rows.append((slot, i, f"{rec['agent_transcript']}\n{utt}", ROLE_CUSTOMER, True))
+                    else:
+                        rows.append((slot, i, utt, ROLE_CUSTOMER, False))
+                else:
+                    slot = self.slots.get(cid, pinned)
+                    rows.append((slot, i, data["transcript"], ROLE_AGENT if kind == "agent" else ROLE_CUSTOMER, False))
+            # the batch contract: a slot's rows contiguous, in arrival order
+            first: Dict[int, int] = {}
+            for k, r in enumerate(rows):
+                first.setdefault(r[0], k)
+            order = sorted(range(len(rows)), key=lambda k: (first[rows[k][0]], k))
+            rows = [rows[k] for k in order]
+            try:
+                res = self._run([_enc(r[2]) for r in rows], [r[0] for r in rows], [r[3] for r in rows],
+                                [now] * len(rows))
+            except PiiError as e:
+                for slot, i, text, role, split_last in rows:
+                    kind, data = reqs[i]
+                    if kind == "agent":
+                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_stored": False}, 200)
+                    elif kind == "customer":
+                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_used": False}, 200)
+                    else:                                   # main.py:458-461 on the error string
+                        red = error_string(e.code, text)
+                        lines = red.splitlines() if split_last else [red]
+                        out[i] = ({"redacted_utterance": lines[-1] if lines else ""}, 200)
+                return
+            for k, (slot, i, text, role, split_last) in enumerate(rows):
+                kind, data = reqs[i]
+                red = _dec(res.text(k))
+                g = int(res.ctx_info[k])
+                if kind == "agent":
+                    if g >= 0:
+                        self.agent_text[slot] = (text, now)
+                    out[i] = ({"redacted_transcript": red, "context_stored": g >= 0}, 200)
+                elif kind == "customer":
+                    out[i] = ({"redacted_transcript": red, "context_used": g >= 0}, 200)
+                else:
+                    if split_last:
+                        lines = red.splitlines()
+                        red = lines[-1] if lines else ""
+                    out[i] = ({"redacted_utterance": red}, 200)
 
     # ---------------------------------------------------------------- aggregator re-scan (a12)
     def rescan_window_batch(self, rows: Sequence[dict], window_n: int = 5, slot_bytes: int = 8192) -> List[str]:
         """Rows as process_batch (original text) -> per row the redacted window
         "\\n".join(last window_n utterances of its conversation), re-scanned with the conversation's
         current expected_pii_type.  Agent rows update the context as handle_agent_utterance does."""
-        texts, slots, roles, ts = [], [], [], []
         with self.lock:
             if getattr(self.engine, "window_n", 0) == 0:
                 self.engine.window_enable(window_n, slot_bytes)
             elif self.engine.window_n != window_n:
                 raise ValueError(f"window already enabled with N={self.engine.window_n}")
-            for r in rows:
-                texts.append(_enc(r["text"]))
-                slots.append(self.slots.get(r["conversation_id"]))
-                pr = str(r.get("participant_role", "")).upper()
-                roles.append(ROLE_AGENT if pr == "AGENT" else ROLE_CUSTOMER if pr in ("END_USER", "CUSTOMER")
-                             else ROLE_OTHER)
-                ts.append(int(r.get("start_timestamp_usec", self._now_us())))
-            res = self.engine.rescan_window(texts, slots, roles, ts)
-            return [_dec(res.text(i)) for i in range(len(rows))]
+        out: List[str] = []
+        for run in self._sub_batches([r["conversation_id"] for r in rows]):
+            with self.lock:
+                now = self._now_us()
+                part = [rows[i] for i in run]
+                pinned = {r["conversation_id"] for r in part}
+                texts = [_enc(r["text"]) for r in part]
+                slots = [self.slots.get(r["conversation_id"], pinned) for r in part]
+                roles = [role_code(r.get("participant_role")) for r in part]
+                ts = [self._row_ts(r, now) for r in part]
+                try:
+                    res = self.engine.rescan_window(texts, slots, roles, ts)
+                except PiiError as e:
+                    out.extend(error_string(e.code, r["text"]) for r in part)
+                    continue
+                for i, r in enumerate(part):
+                    if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
+                        self.agent_text[slots[i]] = (r["text"], ts[i])
+                out.extend(_dec(res.text(i)) for i in range(len(part)))
+        return out
 
     def conversation_ended(self, conversation_id) -> None:
-        """/conversation-ended: the conversation's window and context are dropped."""
+        """/conversation-ended: the conversation's window, its context record (Redis
+        context:{id}) and its host-side agent transcript are dropped and its slot is freed."""
         with self.lock:
-            slot = self.slots.peek(conversation_id)
-            if slot is not None and getattr(self.engine, "window_n", 0):
-                self.engine.window_reset(slot)
+            slot = self.slots.release(conversation_id)
+            if slot is not None:
+                self._evict(slot)
 
     # ---------------------------------------------------------------- batched ingest
     def process_batch(self, rows: Sequence[dict]) -> List[str]:
         """Pub/Sub-shaped rows {conversation_id, participant_role ('AGENT' | 'END_USER' | ...),
         text, start_timestamp_usec}, grouped by conversation in entry order -> redacted texts.
-        Agent rows update their conversation's context exactly as handle_agent_utterance would."""
-        texts, slots, roles, ts = [], [], [], []
-        with self.lock:
-            for r in rows:
-                texts.append(_enc(r["text"]))
-                slots.append(self.slots.get(r["conversation_id"]))
-                pr = str(r.get("participant_role", "")).upper()
-                roles.append(ROLE_AGENT if pr == "AGENT" else ROLE_CUSTOMER if pr in ("END_USER", "CUSTOMER")
-                             else ROLE_OTHER)
-                ts.append(int(r.get("start_timestamp_usec", self._now_us())))
-            res = self._run(texts, slots, roles, ts)
-            for i, r in enumerate(rows):
-                if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
-                    self.agent_text[slots[i]] = (r["text"], ts[i])
-            return [_dec(res.text(i)) for i in range(len(rows))]
+        Agent rows update their conversation's context exactly as handle_agent_utterance would;
+        other roles are redacted without context.  Never raises for engine errors: a failed
+        engine call yields the reference's error strings for its rows (main.py:752-773)."""
+        out: List[str] = []
+        for run in self._sub_batches([r["conversation_id"] for r in rows]):
+            with self.lock:
+                now = self._now_us()
+                part = [rows[i] for i in run]
+                pinned = {r["conversation_id"] for r in part}
+                texts = [_enc(r["text"]) for r in part]
+                slots = [self.slots.get(r["conversation_id"], pinned) for r in part]
+                roles = [role_code(r.get("participant_role")) for r in part]
+                ts = [self._row_ts(r, now) for r in part]
+                try:
+                    res = self._run(texts, slots, roles, ts)
+                except PiiError as e:
+                    out.extend(error_string(e.code, r["text"]) for r in part)
+                    continue
+                for i, r in enumerate(part):
+                    if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
+                        self.agent_text[slots[i]] = (r["text"], ts[i])
+                out.extend(_dec(res.text(i)) for i in range(len(part)))
+        return out
 
     # ---------------------------------------------------------------- Pub/Sub stream formats (§8(f))
     REQUIRED_FIELDS = ("conversation_id", "original_entry_index", "participant_role", "text",
@@ -278,7 +417,10 @@ class PiiService:
         """Raw utterance payloads -> redacted payloads (subscriber_service/main.py:213-221), in input
         order.  A payload missing a required field (subscriber_service/main.py:172-187, same field
         list and emptiness test) or with an empty role yields {"error": "Bad Request", "status": 400}
-        in its place and is not sent to the engine.  Rows are grouped by conversation and ordered by
+        in its place and is not sent to the engine.  A role other than AGENT / END_USER / CUSTOMER
+        is logged and skipped by the reference (subscriber_service/main.py:265-266: nothing is
+        published, the push is acknowledged with 200); it yields {"status": 200, "skipped": ...}
+        here and is not sent to the engine either.  Rows are grouped by conversation and ordered by
         original_entry_index before the engine call (the batch contract), so agent context reaches
         the later customer rows of the same batch exactly as the per-message handlers would."""
         out: List[Optional[dict]] = [None] * len(payloads)
@@ -289,6 +431,10 @@ class PiiService:
             role = str(m.get("participant_role") or "").upper()
             if missing or not role:
                 out[i] = {"error": "Bad Request", "status": 400, "missing_fields": missing}
+                continue
+            if role_code(role) == ROLE_OTHER:
+                out[i] = {"status": 200, "skipped": f"Unknown participant_role: '{role}'",
+                          "conversation_id": m["conversation_id"], "original_entry_index": m["original_entry_index"]}
                 continue
             good.append(i)
         first = {}
@@ -321,7 +467,7 @@ class TranscriptArchive:
 
     def add(self, redacted_payloads: Sequence[dict]) -> None:
         for p in redacted_payloads:
-            if not p or "error" in p:
+            if not p or "error" in p or "skipped" in p:
                 continue
             e = {f: p.get(f) for f in self.FIELDS}
             if p.get("original_text"):
