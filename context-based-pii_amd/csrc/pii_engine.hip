@@ -89,28 +89,95 @@ struct RulesDev {
     uint32_t nl_off;             // tok_bytes[nl_off] = '\n' (the re-scan window separator)
 };
 
-// ------------------------------------------------------------------------------- k_chunk_index
-// first_utt[c] = first utterance starting at or after byte c*BYTES_PER_LANE (c in [0, n_chunks]);
-// also writes every row's defaults (no findings: out_len = len, n_find = 0; keyword group = the
-// always-present group for AGENT rows, else -1) with coalesced stores.
+// ------------------------------------------------------------------------------- lane geometry
+// A scan LANE is the set of utterances whose START lies in one slice [c << sh, (c+1) << sh) of the
+// batch, sliced in the ADDRESS space (positions are shifted by r0 = batch base address & 63, so a
+// slice boundary is a 64-byte boundary of the text buffer).  A LONG row (longer than long_min bytes:
+// a whole transcript, a realtime join, a joined re-scan window) is in addition CUT at every slice
+// boundary strictly inside it, so it is spread over many lanes instead of running on one thread:
+// the lane holding its start ends at the first cut, every further slice is a lane of its own.
+// Lanes are scanned with a halo (k_scan) and stitched by verification (k_scan_fix, k_sel_*).
+struct Geo {
+    const uint64_t* offs;
+    const uint32_t* first_utt;
+    uint64_t base;          // offs[0]
+    uint32_t n_utt, n_chunks, sh, r0, long_min;
+};
+struct Lane {
+    uint32_t lo, hi;        // byte range [lo, hi), batch relative
+    uint32_t u0, u1;        // utterances [u0, u1) overlapping it
+    bool clo, chi;          // cut at lo (continues a long row) / at hi (the long row goes on)
+};
+constexpr uint32_t NO_CUTS = 0xffffffffu;     // long_min that disables cutting (window re-scan)
+constexpr uint32_t SCAN_HALO = 128;            // bytes a lane scans past a cut before it emits
+
+__device__ __forceinline__ int64_t g_off(const Geo& g, uint32_t u) { return (int64_t)(g.offs[u] - g.base); }
+__device__ __forceinline__ int64_t g_cpos(const Geo& g, uint32_t k) { return ((int64_t)k << g.sh) - (int64_t)g.r0; }
+
+// slice boundary k (1 <= k < n_chunks) cuts the row first_utt[k] - 1 (the last row starting before it)
+__device__ __forceinline__ bool g_cut(const Geo& g, uint32_t k) {
+    if (k == 0 || k >= g.n_chunks || g.long_min == NO_CUTS) return false;
+    const uint32_t f = g.first_utt[k];
+    if (f == 0) return false;
+    const int64_t p = g_cpos(g, k), s = g_off(g, f - 1), e = g_off(g, f);
+    return p > s && p < e && (e - s) > (int64_t)g.long_min;
+}
+
+__device__ __forceinline__ Lane g_lane(const Geo& g, uint32_t c) {
+    Lane L;
+    const uint32_t f0 = g.first_utt[c], f1 = g.first_utt[c + 1];
+    L.clo = g_cut(g, c);
+    L.chi = g_cut(g, c + 1);
+    L.lo = (uint32_t)(L.clo ? g_cpos(g, c) : g_off(g, f0));
+    L.hi = (uint32_t)(L.chi ? g_cpos(g, c + 1) : g_off(g, f1));
+    L.u0 = L.clo ? f0 - 1 : f0;
+    L.u1 = f1;
+    return L;
+}
+
+// the lane's event arena starts here (capacity >= its emitted positions + utterance starts, see
+// k_scan); its findings arena at fd + lo / min_len + c
+__device__ __forceinline__ uint64_t ev_base(const Lane& L, uint32_t c) {
+    return (uint64_t)L.lo + c + L.u0 + (L.clo ? 1u : 0u);
+}
+
+// the lanes of cut row r: ca holds its start, (ca, kb] continue it
+__device__ __forceinline__ void row_lanes(const Geo& g, uint32_t r, uint32_t& ca, uint32_t& kb, int64_t& s_r,
+                                          int64_t& e_r) {
+    s_r = g_off(g, r);
+    e_r = g_off(g, r + 1);
+    ca = (uint32_t)((s_r + g.r0) >> g.sh);                                         // lane holding the start
+    kb = (uint32_t)min<int64_t>((int64_t)g.n_chunks - 1, (e_r + g.r0 - 1) >> g.sh);   // last continuation
+}
+
+// first_utt[c] = first utterance starting at or after slice c (c in [0, n_chunks]); also writes every
+// row's defaults (no findings: out_len = len; keyword group = the always-present group for AGENT rows,
+// else -1) with coalesced stores, and lists the rows that will be cut (long rows).
 __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role, uint32_t n_utt,
-                              uint32_t n_chunks, uint32_t lane_shift, int kw_always, uint32_t* __restrict__ first_utt,
-                              uint32_t* __restrict__ out_len, uint32_t* __restrict__ n_find,
-                              int16_t* __restrict__ kw, uint32_t* __restrict__ wc_n) {
+                              uint32_t n_chunks, uint32_t lane_shift, uint32_t r0, uint32_t long_min, int kw_always,
+                              uint32_t* __restrict__ first_utt, uint32_t* __restrict__ out_len,
+                              int32_t* __restrict__ kw, uint32_t* __restrict__ wc_n,
+                              uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u > n_utt) return;
     const uint64_t base = offs[0];
-    const uint64_t su = offs[u] - base;
+    const uint64_t su = offs[u] - base + r0;
     uint64_t c_lo = 0;
-    if (u > 0) c_lo = ((offs[u - 1] - base) >> lane_shift) + 1;
+    if (u > 0) c_lo = ((offs[u - 1] - base + r0) >> lane_shift) + 1;
     uint64_t c_hi = (u == n_utt) ? n_chunks : su >> lane_shift;
     if (c_hi > n_chunks) c_hi = n_chunks;
     for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
     if (u < n_utt) {
-        out_len[u] = (uint32_t)(offs[u + 1] - offs[u]);
-        n_find[u] = 0;
-        kw[u] = (int16_t)((role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1);
+        const uint64_t len = offs[u + 1] - offs[u];
+        out_len[u] = (uint32_t)len;
+        kw[u] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
         if (wc_n) wc_n[u] = 0;
+        // a row that some slice boundary cuts (same test as g_cut)
+        if (long_min != NO_CUTS && len > long_min) {
+            const uint64_t k = ((offs[u] - base + r0) >> lane_shift) + 1;      // first boundary after its start
+            if (k < n_chunks && ((int64_t)(k << lane_shift) - (int64_t)r0) < (int64_t)(offs[u + 1] - base))
+                long_rows[atomicAdd(long_count, 1u)] = u;
+        }
     }
 }
 
@@ -132,44 +199,44 @@ __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
     return (x >> ((K & 3) * 8)) & 0xffu;
 }
 
-// Utterance-start words, lane-interleaved: word[i * n_lanes + c] holds, for lane c's i-th block from
-// the top (aligned 64-byte block b_hi(c) - i, b = (position + mis) >> 6, mis = text address & 63),
-// bit k <=> a non-empty utterance starts at position 64b - mis + k; the lane's top block also carries
-// the bit of the position after its range (the next lane's first start / the batch end), which
-// resets the automata before the lane's last byte.  All lanes of a wavefront read word i at the same
-// iteration, so the scan's word loads are coalesced.  Blocks past LANE_WORDS use a slow path.
+// Utterance-start words, lane-interleaved: word[i * n_lanes + t] holds, for the lane in scan slot t,
+// its i-th block from the top (address-aligned 64-byte block b_top - i, b = (position + r0) >> 6):
+// bit k <=> a non-empty utterance of the lane starts at position 64b - r0 + k, or that position is
+// the lane's scan TOP (the position after its last scanned byte: the next lane's first start, the
+// batch end, or the end of a cut lane's halo), which resets the automata before the lane's last
+// byte.  All lanes of a wavefront read word i at the same iteration, so the scan's word loads are
+// coalesced.  Blocks past LANE_WORDS use a slow path.
 constexpr int LANE_WORDS = 32;
 
-__device__ __forceinline__ void lane_range(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
-                                           uint32_t c, uint32_t& u0, uint32_t& u1, int64_t& lo, int64_t& hi) {
-    u0 = first_utt[c];
-    u1 = first_utt[c + 1];
-    lo = (int64_t)offs[u0];
-    hi = (int64_t)offs[u1] - 1;
+// exclusive end of the bytes lane L scans: its range, plus a halo past a cut (clamped to the row)
+__device__ __forceinline__ uint32_t scan_top(const Geo& g, const Lane& L) {
+    if (!L.chi) return L.hi;
+    return (uint32_t)min<int64_t>((int64_t)L.hi + SCAN_HALO, g_off(g, L.u1));
 }
 
-// bits of lane c's i-th block from the top (the slow path for i >= LANE_WORDS: binary search + walk
-// over offs; everything is re-derived from (c, i) so the scan keeps nothing live for it)
-__device__ __attribute__((noinline)) uint64_t block_bits_slow(const uint64_t* __restrict__ offs,
-                                                              const uint32_t* __restrict__ first_utt, uint32_t c,
-                                                              uint32_t i, int64_t mis) {
-    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
-    const int64_t b_hi = ((int64_t)offs[u1] - 1 + mis) >> 6;
-    const int64_t blk = b_hi - i;
-    const int64_t plo = blk * 64 - mis, phi = plo + 64;       // positions [plo, phi)
-    // largest u in [u0, u1] with offs[u] < phi
-    uint32_t a = u0, b = u1;
+// bits of lane c's i-th block from the top (the slow path for i >= LANE_WORDS: binary search over the
+// lane's utterances; everything is re-derived from (c, i) so the scan keeps nothing live for it)
+__device__ __attribute__((noinline)) uint64_t block_bits_slow(const Geo g, uint32_t c, uint32_t i) {
+    const Lane L = g_lane(g, c);
+    const uint32_t top = scan_top(g, L);
+    const int64_t blk = (((int64_t)top - 1 + g.r0) >> 6) - i;
+    const int64_t plo = blk * 64 - g.r0, phi = plo + 64;       // positions [plo, phi)
+    uint64_t bits = 0;
+    if ((int64_t)top >= plo && (int64_t)top < phi) bits |= 1ull << (top - plo);
+    const uint32_t vmin = L.u0 + (L.clo ? 1u : 0u);
+    if (vmin >= L.u1) return bits;
+    // largest v in [vmin, u1) with start < phi
+    uint32_t a = vmin, b = L.u1 - 1;
+    if (g_off(g, a) >= phi) return bits;
     while (a < b) {
         const uint32_t m = (a + b + 1) >> 1;
-        if ((int64_t)offs[m] < phi) a = m;
+        if (g_off(g, m) < phi) a = m;
         else b = m - 1;
     }
-    uint64_t bits = 0;
-    for (int64_t u = a; u >= (int64_t)u0; --u) {
-        const int64_t su = (int64_t)offs[u];
-        if (su < plo) break;
-        const bool reset = u == (int64_t)u1;                   // the position after the lane's range
-        if ((reset && blk == b_hi) || (!reset && (int64_t)offs[u + 1] > su)) bits |= 1ull << (su - plo);
+    for (int64_t v = a; v >= (int64_t)vmin; --v) {
+        const int64_t sv = g_off(g, (uint32_t)v);
+        if (sv < plo) break;
+        if (g_off(g, (uint32_t)v + 1) > sv) bits |= 1ull << (sv - plo);
     }
     return bits;
 }
@@ -183,32 +250,28 @@ __device__ __attribute__((noinline)) uint64_t block_bits_slow(const uint64_t* __
 // reservations race) but only the thread mapping depends on it: every lane's events, counts and
 // arena are the same.
 constexpr int LANE_NB = 128;                       // length buckets: 0 = longest (>= 127*32 B)
-__device__ __forceinline__ uint32_t lane_bucket(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ first_utt,
-                                                uint32_t c) {
-    const uint64_t len = offs[first_utt[c + 1]] - offs[first_utt[c]];
-    return (uint32_t)(LANE_NB - 1) - (uint32_t)min<uint64_t>(len >> 5, LANE_NB - 1);
+__device__ __forceinline__ uint32_t lane_bucket(const Geo& g, uint32_t c) {
+    const Lane L = g_lane(g, c);
+    const uint32_t len = scan_top(g, L) - min(L.lo, scan_top(g, L));
+    return (uint32_t)(LANE_NB - 1) - min<uint32_t>(len >> 5, LANE_NB - 1);
 }
 
 constexpr uint32_t LANE_SORT_CHUNK = 4096;         // lanes per workgroup (few global reservations)
 
-__global__ __launch_bounds__(256) void k_lane_count(const uint64_t* __restrict__ offs,
-                                                    const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                    uint32_t* __restrict__ bucket_cnt) {
+__global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __restrict__ bucket_cnt) {
     __shared__ uint32_t h[LANE_NB];
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK, c1 = min(c0 + LANE_SORT_CHUNK, n_chunks);
-    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) atomicAdd(&h[lane_bucket(offs, first_utt, c)], 1u);
+    const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK, c1 = min(c0 + LANE_SORT_CHUNK, g.n_chunks);
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) atomicAdd(&h[lane_bucket(g, c)], 1u);
     __syncthreads();
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
         if (h[i]) atomicAdd(&bucket_cnt[i], h[i]);
 }
 
 // bucket_cnt[0..NB) = counts (k_lane_count), bucket_cnt[NB..2NB) = reservation cursors (zeroed)
-__global__ __launch_bounds__(256) void k_lane_place(const uint64_t* __restrict__ offs,
-                                                    const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                    uint32_t* __restrict__ bucket_cnt, uint32_t* __restrict__ lane_perm,
-                                                    uint32_t* __restrict__ lane_pos) {
+__global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __restrict__ bucket_cnt,
+                                                    uint32_t* __restrict__ lane_perm, uint32_t* __restrict__ lane_pos) {
     constexpr int PER = LANE_SORT_CHUNK / 256;
     __shared__ uint32_t base[LANE_NB], h[LANE_NB];
     if (threadIdx.x < 64) {                        // exclusive prefix of the counts, one wavefront
@@ -231,8 +294,8 @@ __global__ __launch_bounds__(256) void k_lane_place(const uint64_t* __restrict__
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t c = c0 + j * 256 + threadIdx.x;
-        bk[j] = c < n_chunks ? lane_bucket(offs, first_utt, c) : 0u;
-        rk[j] = c < n_chunks ? atomicAdd(&h[bk[j]], 1u) : 0u;
+        bk[j] = c < g.n_chunks ? lane_bucket(g, c) : 0u;
+        rk[j] = c < g.n_chunks ? atomicAdd(&h[bk[j]], 1u) : 0u;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
@@ -241,7 +304,7 @@ __global__ __launch_bounds__(256) void k_lane_place(const uint64_t* __restrict__
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t c = c0 + j * 256 + threadIdx.x;
-        if (c < n_chunks) {
+        if (c < g.n_chunks) {
             const uint32_t t = base[bk[j]] + rk[j];
             lane_perm[t] = c;
             lane_pos[c] = t;
@@ -250,45 +313,42 @@ __global__ __launch_bounds__(256) void k_lane_place(const uint64_t* __restrict__
 }
 
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
-__global__ __launch_bounds__(256) void k_lane_bits(const uint64_t* __restrict__ offs,
-                                                   const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
-                                                   int64_t mis, const uint32_t* __restrict__ lane_pos,
+__global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* __restrict__ lane_pos,
                                                    uint64_t* __restrict__ words) {
     __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t cw0 = c - lane;
-    const uint32_t cw1 = min(cw0 + 64, n_chunks);
-    const uint32_t U0 = cw0 < n_chunks ? first_utt[cw0] : 0u;
-    const uint32_t U1 = cw0 < n_chunks ? first_utt[cw1] : 0u;
+    const uint32_t cw1 = min(cw0 + 64, g.n_chunks);
+    // the wavefront's utterances [U0, U1] (one before its first lane's first start: a cut row)
+    const uint32_t U0 = cw0 < g.n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
+    const uint32_t U1 = cw0 < g.n_chunks ? min(g.first_utt[cw1] + 1u, g.n_utt) : 0u;
     const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
     int64_t* so = s_off[wv];
-    if (staged && cw0 < n_chunks)
-        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (int64_t)offs[U0 + k];
+    if (staged && cw0 < g.n_chunks)
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = g_off(g, U0 + k);
     __syncthreads();
-    if (c >= n_chunks) return;
-    auto uoff = [&](int64_t u) { return staged ? so[u - U0] : (int64_t)offs[u]; };
-    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
-    const int64_t lo = uoff(u0), hi = uoff(u1) - 1;
-    if (hi < lo) return;
-    const int64_t b_hi = (hi + mis) >> 6, b_lo = (lo + mis) >> 6;
+    if (c >= g.n_chunks) return;
+    auto uoff = [&](int64_t u) { return staged ? so[u - U0] : g_off(g, (uint32_t)u); };
+    const Lane L = g_lane(g, c);
+    const uint32_t top = scan_top(g, L);
+    if (top <= L.lo) return;
+    const int64_t b_hi = ((int64_t)top - 1 + g.r0) >> 6, b_lo = ((int64_t)L.lo + g.r0) >> 6;
     const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
     const uint32_t slot = lane_pos[c];
-    int64_t u = u1;
-    int64_t su = uoff(u);
+    const int64_t vmin = (int64_t)L.u0 + (L.clo ? 1 : 0);
+    int64_t v = (int64_t)L.u1 - 1;
+    int64_t sv = v >= vmin ? uoff(v) : 0;
     for (int64_t i = 0; i < nw; ++i) {
-        const int64_t blk = b_hi - i;
-        const int64_t plo = blk * 64 - mis;
+        const int64_t plo = (b_hi - i) * 64 - g.r0;
         uint64_t bits = 0;
-        while (u >= (int64_t)u0 && su >= plo) {
-            if (su < plo + 64) {
-                const bool reset = u == (int64_t)u1;
-                if ((reset && i == 0) || (!reset && uoff(u + 1) > su)) bits |= 1ull << (su - plo);
-            }
-            --u;
-            if (u >= (int64_t)u0) su = uoff(u);
+        if (i == 0 && (int64_t)top >= plo && (int64_t)top < plo + 64) bits |= 1ull << (top - plo);
+        while (v >= vmin && sv >= plo) {
+            if (sv < plo + 64 && uoff(v + 1) > sv) bits |= 1ull << (sv - plo);
+            --v;
+            if (v >= vmin) sv = uoff(v);
         }
-        words[(uint64_t)i * n_chunks + slot] = bits;
+        words[(uint64_t)i * g.n_chunks + slot] = bits;
     }
 }
 
@@ -300,7 +360,8 @@ __device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
     return *reinterpret_cast<lds_u16_t*>((size_t)addr);
 }
 
-// the lane's events go to ev[lo_r ...] (its own arena: a lane never has more events than bytes + 1)
+// the lane's events go to its own arena (ev_base): only positions in its emission range [lo_r,
+// lo_r + len_r] are recorded
 __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt, uint32_t pos, uint32_t lo_r,
                                           uint32_t len_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
     if (pos - lo_r <= len_r) {
@@ -308,7 +369,7 @@ __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt,
         e.pos = (uint32_t)pos;
         e.sd = (uint16_t)((ad - SCAN_TD_BASE) >> 1);     // transition index (row * CD + class)
         e.sk = (uint16_t)((ak - tk_base) >> 1);
-        ev[(uint64_t)lo_r + cnt++] = e;
+        ev[cnt++] = e;
     }
 }
 
@@ -379,7 +440,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
         SCAN_STEP8(7, H) SCAN_STEP8(6, H) SCAN_STEP8(5, H) SCAN_STEP8(4, H)                       \
         SCAN_STEP8(3, H) SCAN_STEP8(2, H) SCAN_STEP8(1, H) SCAN_STEP8(0, H)                       \
         if (__builtin_expect(m != 0, 0))                                                          \
-            scan_emit8(ev, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
+            scan_emit8(arena, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
     }
 
 #define SCAN_SUB(W, OFF)                                                                          \
@@ -389,12 +450,22 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
         SCAN_GROUP8(W, 0, OFF)                                                                    \
     }
 
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uint8_t* __restrict__ text,
-                                                     const uint64_t* __restrict__ offs, uint32_t n_utt,
-                                                     const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+// the state a lane carries across a cut: both automata's current rows (flag bits masked off)
+__device__ __forceinline__ uint32_t scan_state(uint32_t nd, uint32_t nk) { return (nd & 0xfffcu) | ((nk & 0xfffcu) << 16); }
+
+// Emission range of lane L: event positions [e_lo, e_hi].  A position is reported by the step over the
+// byte before it, so a lane cut at lo leaves position lo to its left neighbour, and a lane cut at hi
+// reports position hi itself (the right neighbour never steps byte hi - 1).
+__device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32_t& e_len) {
+    e_lo = L.lo + (L.clo ? 1u : 0u);
+    const uint32_t e_hi = L.chi ? L.hi : L.hi - 1u;
+    e_len = e_hi - e_lo;                 // wraps for an empty range: nothing is emitted
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
-                                                     uint32_t* __restrict__ lane_cnt) {
+                                                     uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
     const int nd_words = R.SD * R.CDs / 2;      // rows padded to an even class count
@@ -411,28 +482,27 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
     }
     __syncthreads();
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
-    if (t >= n_chunks) return;
+    if (t >= g.n_chunks) return;
     const uint32_t c = lane_perm[t];
-    const uint32_t u0 = first_utt[c], u1 = first_utt[c + 1];
-    const uint64_t base = offs[0];
+    const Lane L = g_lane(g, c);
     // positions relative to the batch base fit 32 bits (PII_MAX_BATCH_BYTES); 32-bit arithmetic keeps
     // the lane's bookkeeping small (VGPRs decide this kernel's occupancy)
-    const uint32_t lo_r = (uint32_t)(offs[u0] - base);      // lane range [lo_r, hi_r]
-    const uint32_t hi_r = (uint32_t)(offs[u1] - base) - 1u;
-    const uint32_t end_r = (uint32_t)(offs[n_utt] - base);
+    const uint32_t top = scan_top(g, L);
+    const uint32_t end_r = (uint32_t)g_off(g, g.n_utt);
     uint32_t cnt = 0;
-    if (offs[u1] > offs[u0]) {
-        const uint32_t len_r = hi_r - lo_r;
+    if (top > L.lo) {
+        uint32_t lo_r, len_r;
+        emit_range(L, lo_r, len_r);
+        Event* __restrict__ arena = ev + ev_base(L, c);
         const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
         const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
         const uint32_t start2 = d_start | (k_start << 16);
         uint32_t nd = 0, nk = 0, pm = 0xffffffffu;     // "previous byte started an utterance": start rows
         // aligned 64-byte blocks of the ADDRESS space, numbered from the one holding the batch base:
         // block bb covers relative positions [64 bb - r0, 64 bb - r0 + 64)
-        const uintptr_t abase = (uintptr_t)(text + base);
-        const uint32_t r0 = (uint32_t)(abase & 63);
-        const uintptr_t tpb = abase - r0;                           // global loads (see gload16)
-        const uint32_t bb_hi = (hi_r + r0) >> 6, bb_lo = (lo_r + r0) >> 6;
+        const uint32_t r0 = g.r0;
+        const uintptr_t tpb = (uintptr_t)(text + g.base) - r0;      // global loads (see gload16)
+        const uint32_t bb_hi = (top - 1 + r0) >> 6, bb_lo = (L.lo + r0) >> 6;
         // the top block: only chunks holding a batch byte are read (the rest step as zero bytes
         // before the end-of-batch / next-utterance reset)
         const uint32_t q_end = (end_r - 1 + r0) >> 4;               // last chunk with a batch byte
@@ -451,18 +521,149 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const uin
                 n2 = gload16(q + 32);
                 n3 = gload16(q + 48);
                 const uint32_t i = bb_hi - (bb - 1);
-                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * n_chunks + t]
-                                              : block_bits_slow(offs, first_utt, c, i, (int64_t)((uintptr_t)text & 63));
+                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * g.n_chunks + t] : block_bits_slow(g, c, i);
             }
             const uint32_t bpos = 64u * bb - r0;        // relative position of the block's byte 0 (mod 2^32)
             SCAN_SUB(w3, 48)
             SCAN_SUB(w2, 32)
             SCAN_SUB(w1, 16)
             SCAN_SUB(w0, 0)
+            // a lane cut at hi: the state its halo produced for the byte before hi (k_scan_fix checks it
+            // against the state the right neighbour ends with)
+            if (L.chi && bpos == L.hi) lane_st[2 * c] = scan_state(nd, nk);
             if (bb == bb_lo) break;
+        }
+        if (L.clo) lane_st[2 * c + 1] = scan_state(nd, nk);        // lo is block aligned: state after byte lo
+    }
+    lane_cnt[c] = cnt;
+}
+
+// ---- k_scan_fix: stitching of cut rows.  A lane cut at hi scanned SCAN_HALO bytes past the cut from
+// the start state; when that did not reproduce the state its right neighbour really ends with (a
+// context longer than the halo: a long unbroken token), the lane is re-scanned from the true state.
+// One workgroup per cut row: check every boundary, re-scan the mismatches (each from its right
+// neighbour's state, which the same round may not change), then re-check only the boundaries left of
+// a re-scanned lane until nothing changes.  Re-scans are rare and sequential per lane.
+__device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __restrict__ text, uint32_t c,
+                            uint32_t entry, Event* __restrict__ ev, uint32_t* __restrict__ lane_cnt,
+                            uint32_t* __restrict__ lane_st) {
+    const uint32_t* s_cmap = nullptr;        // LDS address 0 (k_scan layout)
+    (void)s_cmap;
+    const Lane L = g_lane(g, c);
+    uint32_t lo_r, len_r;
+    emit_range(L, lo_r, len_r);
+    Event* __restrict__ arena = ev + ev_base(L, c);
+    const uint32_t nd_words = (uint32_t)(R.SD * R.CDs / 2);
+    const uint32_t tk_base = SCAN_TD_BASE + nd_words * 4;
+    const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
+    const uint32_t start2 = (uint32_t)R.d_start | ((uint32_t)R.k_start << 16);
+    const uint8_t* tb = text + g.base;
+    uint32_t nd = entry & 0xffffu, nk = entry >> 16, pm = 0;
+    uint32_t cnt = 0;
+    // utterance starts inside the lane, walked downwards
+    const int64_t vmin = (int64_t)L.u0 + (L.clo ? 1 : 0);
+    int64_t v = (int64_t)L.u1 - 1;
+    while (v >= vmin && (g_off(g, (uint32_t)v) >= (int64_t)L.hi || g_off(g, (uint32_t)v + 1) == g_off(g, (uint32_t)v)))
+        --v;
+    for (int64_t b = (int64_t)L.hi - 1; b >= (int64_t)L.lo; --b) {
+        const uint32_t cls = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)(4u * tb[b]));
+        const uint32_t x = cls + (pm & start2);
+        const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
+        const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
+        nd = lds_u16(ad);
+        nk = lds_u16(ak);
+        const bool st = v >= vmin && g_off(g, (uint32_t)v) == b;
+        pm = st ? 0xffffffffu : 0u;
+        if ((nd | nk) & 1u) scan_emit(arena, cnt, (uint32_t)b + 1u, lo_r, len_r, ad, ak, tk_base);
+        if (st) {
+            if ((nd | nk) & 2u)
+                scan_emit(arena, cnt, (uint32_t)b, lo_r, len_r, (nd & 0xfffcu) + eot_d, (nk & 0xfffcu) + eot_k, tk_base);
+            --v;
+            while (v >= vmin && g_off(g, (uint32_t)v + 1) == g_off(g, (uint32_t)v)) --v;     // empty rows
         }
     }
     lane_cnt[c] = cnt;
+    lane_st[2 * c] = entry;
+    if (L.clo) lane_st[2 * c + 1] = scan_state(nd, nk);
+}
+
+constexpr int FIX_Q = 512;
+
+__global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+                                                  const uint32_t* __restrict__ long_rows,
+                                                  const uint32_t* __restrict__ long_count, Event* __restrict__ ev,
+                                                  uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+    __shared__ uint32_t s_q[FIX_Q], s_e[FIX_Q], s_prev[FIX_Q];
+    __shared__ uint32_t s_n, s_np, s_full;
+    const uint32_t nrows = *long_count;
+    if (blockIdx.x >= nrows) return;
+    {
+        const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
+        const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
+        const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
+        uint32_t* d_td = smem32 + 256;
+        uint32_t* d_tk = d_td + nd_words;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
+        for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
+        for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
+    }
+    __syncthreads();
+    for (uint32_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+        uint32_t ca, kb;
+        int64_t s_r, e_r;
+        row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
+        // boundaries c | c + 1 for c in [ca, kb); round 1 checks all of them
+        bool all = true;
+        for (;;) {
+            if (threadIdx.x == 0) {
+                s_n = 0;
+                s_full = 0;
+            }
+            __syncthreads();
+            if (all) {
+                for (uint32_t c = ca + threadIdx.x; c < kb; c += blockDim.x) {
+                    const uint32_t want = lane_st[2 * (c + 1) + 1];
+                    if (lane_st[2 * c] != want) {
+                        const uint32_t k = atomicAdd(&s_n, 1u);
+                        if (k < FIX_Q) {
+                            s_q[k] = c;
+                            s_e[k] = want;
+                        } else {
+                            s_full = 1;
+                        }
+                    }
+                }
+            } else {
+                for (uint32_t k = threadIdx.x; k < s_np; k += blockDim.x) {
+                    const uint32_t c = s_prev[k];
+                    if (c <= ca) continue;
+                    const uint32_t b = c - 1;           // its left boundary: lane c's state changed
+                    const uint32_t want = lane_st[2 * c + 1];
+                    if (lane_st[2 * b] != want) {
+                        const uint32_t q = atomicAdd(&s_n, 1u);
+                        if (q < FIX_Q) {
+                            s_q[q] = b;
+                            s_e[q] = want;
+                        } else {
+                            s_full = 1;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            const uint32_t n = min(s_n, (uint32_t)FIX_Q);
+            if (n == 0 && !s_full) break;
+            for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
+                rescan_lane(R, g, text, s_q[k], s_e[k], ev, lane_cnt, lane_st);
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) s_prev[k] = s_q[k];
+            if (threadIdx.x == 0) s_np = n;
+            all = s_full != 0;                          // an overflowed round re-checks everything
+            __syncthreads();
+        }
+        __syncthreads();
+    }
 }
 #undef SCAN_STEP8
 #undef SCAN_GROUP8
@@ -483,7 +684,7 @@ __device__ __forceinline__ SegV seg_combine(SegV a, SegV b) {
 }
 
 __global__ __launch_bounds__(CTX_BLOCK) void k_ctx_scan(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
-                                                        const int16_t* __restrict__ kw, uint32_t n_utt, uint32_t n_slots,
+                                                        const int32_t* __restrict__ kw, uint32_t n_utt, uint32_t n_slots,
                                                         uint32_t* __restrict__ incl, int32_t* __restrict__ agg_v,
                                                         uint32_t* __restrict__ agg_f, uint32_t* __restrict__ stamp,
                                                         uint32_t epoch, uint32_t* __restrict__ err) {
@@ -533,7 +734,7 @@ __device__ __forceinline__ int32_t ctx_carry(const int32_t* agg_v, const uint32_
 }
 
 __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
-                            const int16_t* __restrict__ kw, const int64_t* __restrict__ ts, uint32_t n_utt,
+                            const int32_t* __restrict__ kw, const int64_t* __restrict__ ts, uint32_t n_utt,
                             uint32_t n_slots, int64_t ttl_us, const uint32_t* __restrict__ incl,
                             const int32_t* __restrict__ agg_v, const uint32_t* __restrict__ agg_f,
                             const int32_t* __restrict__ st_group, const int64_t* __restrict__ st_ts,
@@ -571,8 +772,8 @@ __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __
     }
     // the re-scan window of row u uses the context a request right after u would GET (main.py:403):
     // an AGENT row's own hit, else the live record
-    if (win_ctx) win_ctx[u] = (r == PII_ROLE_AGENT && kw[u] >= 0) ? kw[u] : live;
-    ctx[u] = (r == PII_ROLE_AGENT) ? kw[u] : used;
+    if (win_ctx) win_ctx[u] = (r == PII_ROLE_AGENT && kw[u] >= 0) ? (int16_t)kw[u] : live;
+    ctx[u] = (r == PII_ROLE_AGENT) ? (int16_t)kw[u] : used;
     // last row of the run: the latest hit of the whole run (to be committed)
     const bool last = (u == n_utt - 1) || slot[u + 1] != sl;
     if (last) {
@@ -581,7 +782,7 @@ __global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __
     }
 }
 
-__global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int16_t* __restrict__ kw,
+__global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int32_t* __restrict__ kw,
                              const int64_t* __restrict__ ts, uint32_t n_utt, uint32_t n_slots,
                              const int32_t* __restrict__ commit, const uint32_t* __restrict__ err,
                              int32_t* __restrict__ st_group, int64_t* __restrict__ st_ts) {
@@ -665,10 +866,9 @@ constexpr int PAIRS_BLOCK = 256;
 // an exclusive scan of the counts gives every lane its block of the queue (lane order, no atomics),
 // WRITE = true fills the blocks.
 template <bool WRITE>
-__global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const uint64_t* __restrict__ offs,
-                                               const uint32_t* __restrict__ first_utt, uint32_t n_chunks,
+__global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const Geo g,
                                                const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
-                                               const uint8_t* __restrict__ role, int16_t* __restrict__ kw,
+                                               const uint8_t* __restrict__ role, int32_t* __restrict__ kw,
                                                EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
                                                uint64_t pair_cap, uint64_t ev_cap,
                                                const uint64_t* __restrict__ lane_pair,
@@ -680,17 +880,19 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const u
     __shared__ uint16_t s_kmin[256];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t n_chunks = g.n_chunks;
     const bool valid = c < n_chunks;
-    const int64_t base = (int64_t)offs[0];
+    const uint64_t* __restrict__ offs = g.offs;
+    const int64_t base = (int64_t)g.base;
     // small accept-set tables (<= 256 sets; larger rule sets read them from global memory)
     const uint32_t n_dacc = R.n_dacc, n_kacc = R.n_kacc;
     for (uint32_t i = threadIdx.x; i <= n_dacc && i < 256; i += PAIRS_BLOCK) s_acc_off[i] = R.d_acc_off[i];
     for (uint32_t i = threadIdx.x; i < n_kacc && i < 256; i += PAIRS_BLOCK) s_kmin[i] = R.k_acc_min[i];
-    // the wavefront's utterances [U0, U1]
+    // the wavefront's utterances [U0, U1] (from one before its first lane's first start: a cut row)
     const uint32_t cw0 = c - lane;
     const uint32_t cw1 = min(cw0 + 64, n_chunks);
-    const uint32_t U0 = cw0 < n_chunks ? first_utt[cw0] : 0u;
-    const uint32_t U1 = cw0 < n_chunks ? first_utt[cw1] : 0u;
+    const uint32_t U0 = cw0 < n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
+    const uint32_t U1 = cw0 < n_chunks ? g.first_utt[cw1] : 0u;
     const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
     uint32_t* so = s_off[wv];
     uint8_t* sr = s_role[wv];
@@ -708,26 +910,35 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const u
     const uint32_t cnt = valid ? lane_cnt[c] : 0u;
     const Event* evl = nullptr;
     int64_t u_top = 0;
+    Lane L{};
     if (cnt) {
-        const uint32_t u0 = first_utt[c];
-        evl = ev + uoff(u0);
-        u_top = (int64_t)first_utt[c + 1] - 1;
+        L = g_lane(g, c);
+        evl = ev + ev_base(L, c);
+        u_top = (int64_t)L.u1 - 1;
     }
     if (!WRITE) {
-        // count pairs, keyword groups of AGENT rows
+        // count pairs, keyword groups of AGENT rows (a cut row's lanes merge theirs with an atomic min:
+        // -1 = no hit is the largest unsigned value)
+        auto put_kw = [&](int64_t u, int grp) {
+            const int v = min(grp, R.kw_always_min);
+            if ((L.clo && u == (int64_t)L.u0) || (L.chi && u == u_top))
+                atomicMin(reinterpret_cast<unsigned int*>(kw + u), (unsigned int)v);
+            else
+                kw[u] = v;
+        };
         uint32_t np = 0;
         int64_t u = u_top;
         int64_t s_u = cnt ? uoff(u) : 0;
         bool agent = cnt ? uagent(u) : false;
-        int g = KW_NONE;
+        int grp = KW_NONE;
         Event En = cnt ? evl[0] : Event{};
         for (uint32_t k = 0; k < cnt; ++k) {
             const Event E = En;
             if (k + 1 < cnt) En = evl[k + 1];      // next event in flight while this one decodes
             const int64_t pos = E.pos;
             while (pos < s_u) {
-                if (g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
-                g = KW_NONE;
+                if (grp != KW_NONE) put_kw(u, grp);
+                grp = KW_NONE;
                 --u;
                 s_u = uoff(u);
                 agent = uagent(u);
@@ -736,10 +947,10 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const u
             np += acc_off(acc + 1) - acc_off(acc);
             if (agent) {
                 const uint32_t a = R.k_accid[E.sk];
-                if (a) g = min(g, (int)kmin(a));
+                if (a) grp = min(grp, (int)kmin(a));
             }
         }
-        if (cnt && g != KW_NONE) kw[u] = (int16_t)min(g, R.kw_always_min);
+        if (cnt && grp != KW_NONE) put_kw(u, grp);
         if (valid) lane_np[c] = np;
         return;
     }
@@ -1029,44 +1240,76 @@ __device__ __forceinline__ uint32_t matched_mask16(int4 c0, int4 c1, int4 c2, in
 
 // Per scan lane: its pairs in (utterance, start, accept-set) order.  Unmatched pairs change no state
 // (finditer skipping, exclusion and overlap only see matches), so only matched ones are decoded.
-__global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
-                                                uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
-                                                const uint32_t* __restrict__ lane_np,
-                                                const EvLoc* __restrict__ evloc, const PairRes* __restrict__ pres,
-                                                const int32_t* __restrict__ pend,
-                                                uint64_t pair_cap, const uint8_t* __restrict__ role,
-                                                const int16_t* __restrict__ ctx, pii_span* __restrict__ fd,
-                                                uint32_t* __restrict__ n_find, uint32_t* __restrict__ out_len,
-                                                const uint32_t* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & ERR_QUEUE) return;           // the batch is re-run with a larger queue
-    const uint8_t* lb = load_image(img, li.total, lds4);
-    const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[SE_DTYPE]);
-    const uint8_t* ven = lb + li.off[SE_VEN];
-    const uint8_t* vmin = lb + li.off[SE_VMIN];
-    const uint8_t* dex = lb + li.off[SE_DEX];
-    const uint32_t* xoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_XOFF]);
-    const uint16_t* xids = reinterpret_cast<const uint16_t*>(lb + li.off[SE_XIDS]);
-    const uint32_t* tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_TOKOFF]);
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
-    const uint32_t np = lane_np[c];
-    if (np == 0 || lane_pair[c] + np > pair_cap) return;     // overflowed queue: the batch is re-run
-    const PairRes* rl = pres + lane_pair[c];
-    const int32_t* el = pend + lane_pair[c];
+// Findings go to the LANE's arena (fd + fd_base), in (utterance, start) order; lane_nf counts them.
+// A whole utterance's output length is written directly; a cut row's findings are split over its
+// lanes, whose deltas (token length - match length) k_rowlen adds up.  A lane that continues a cut
+// row starts with a fresh state, which is exact unless a match of the previous lanes reaches into it
+// (lane_reach); k_sel_dirty / k_sel_fix re-run those lanes with the carried state.
+struct SelTabs {
+    const uint16_t* dtype;
+    const uint8_t* ven;
+    const uint8_t* vmin;
+    const uint8_t* dex;
+    const uint32_t* xoff;
+    const uint16_t* xids;
+    const uint32_t* tokoff;
+};
+struct SelIO {
+    const uint64_t* lane_pair;
+    const uint32_t* lane_np;
+    const EvLoc* evloc;
+    const PairRes* pres;
+    const int32_t* pend;
+    uint64_t pair_cap;
+    const uint8_t* role;
+    const int16_t* ctx;
+    pii_span* fd;
+    uint32_t* lane_nf;
+    int2* lane_rd;          // cut-row deltas: .x = row u0 (lane cut at lo), .y = row u1 - 1 (cut at hi)
+    uint32_t* lane_reach;   // lanes cut at hi: furthest match end of the cut row (row relative)
+    uint32_t* out_len;
+    uint2* spill;           // per pair-queue index: the (pattern, end) list of a run past LIVE patterns
+};
+
+__device__ __forceinline__ uint64_t fd_base(const Lane& L, uint32_t c, int min_len) {
+    return (uint64_t)(L.lo / (uint32_t)min_len) + c;
+}
+
+__device__ __forceinline__ SelTabs sel_tabs(const uint8_t* lb, const LdsImage& li) {
+    SelTabs T;
+    T.dtype = reinterpret_cast<const uint16_t*>(lb + li.off[SE_DTYPE]);
+    T.ven = lb + li.off[SE_VEN];
+    T.vmin = lb + li.off[SE_VMIN];
+    T.dex = lb + li.off[SE_DEX];
+    T.xoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_XOFF]);
+    T.xids = reinterpret_cast<const uint16_t*>(lb + li.off[SE_XIDS]);
+    T.tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_TOKOFF]);
+    return T;
+}
+
+// select over the pairs of lanes c0..c1 as ONE sequential pass (the state carries across the lanes)
+__device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t c0,
+                           uint32_t c1) {
     const int T = R.T;
+    uint2* __restrict__ spill = io.spill + io.lane_pair[c0];
     // per-utterance state
     uint32_t u = 0xffffffffu;
     int v = 0, minlik = 0, L = 0;
-    pii_span* fdu = nullptr;
     int lp[LIVE], le[LIVE];
-    uint32_t cur_s[P_MAX];     // spill array: touched only when LIVE slots overflow
+    uint32_t n_spill = 0;
     bool spilled = false;
     int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
     uint32_t ex_valid = 0;
     int max_end = 0;
-    uint32_t nf = 0;
-    int delta = 0;
+    uint32_t nf_u = 0;
+    int delta_u = 0;
+    // per-lane state
+    Lane Lg{};
+    uint32_t lane = c0;
+    pii_span* fdl = nullptr;
+    uint32_t nfl = 0;
+    int rdx = 0, rdy = 0;
+    uint32_t reach = 0;
     // per-start state
     int s = -1, best_e = -1, best_t = 0, best_lik = 0;
 #pragma unroll
@@ -1074,6 +1317,8 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
         lp[q] = -1;
         le[q] = -1;
     }
+    auto cut_lo_row = [&](uint32_t x) { return Lg.clo && x == Lg.u0; };
+    auto cut_row = [&](uint32_t x) { return cut_lo_row(x) || (Lg.chi && x == Lg.u1 - 1); };
     auto flush_start = [&]() {
         if (best_e >= 0 && s >= max_end) {
             pii_span f;
@@ -1083,21 +1328,24 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
             f.info_type = (uint16_t)best_t;
             f.likelihood = (uint8_t)best_lik;
             f.flags = 0;
-            fdu[nf++] = f;
+            fdl[nfl++] = f;
             max_end = best_e;
-            delta += (int)(tokoff[best_t + 1] - tokoff[best_t]) - (best_e - s);
+            const int d = (int)(Tb.tokoff[best_t + 1] - Tb.tokoff[best_t]) - (best_e - s);
+            if (cut_lo_row(u)) rdx += d;
+            else if (cut_row(u)) rdy += d;
+            else {
+                delta_u += d;
+                ++nf_u;
+            }
         }
         best_e = -1;
     };
     auto flush_utt = [&]() {
-        if (nf) {
-            n_find[u] = nf;
-            out_len[u] = (uint32_t)(L + delta);
-        }
+        if (nf_u) io.out_len[u] = (uint32_t)(L + delta_u);
     };
-    auto pair = [&](uint32_t i, int e) {
-        const PairRes P = rl[i];
-        const EvLoc Lc = evloc[P.ev];
+    auto pair = [&](uint64_t i, int e) {
+        const PairRes P = io.pres[i];
+        const EvLoc Lc = io.evloc[P.ev];
         const int ps = (int)(Lc.s - Lc.ustart);
         if (Lc.u != u) {
             if (u != 0xffffffffu) {
@@ -1105,31 +1353,33 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
                 flush_utt();
             }
             u = Lc.u;
-            v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
-            minlik = vmin[v];
+            v = (io.role[u] == PII_ROLE_CUSTOMER && io.ctx[u] >= 0) ? io.ctx[u] + 1 : 0;
+            minlik = Tb.vmin[v];
             L = (int)(Lc.uend - Lc.ustart);
-            fdu = fd + Lc.ustart / R.min_len;
 #pragma unroll
             for (int q = 0; q < LIVE; ++q) {
                 lp[q] = -1;
                 le[q] = -1;
             }
             spilled = false;
+            n_spill = 0;
             ex_valid = 0;
             max_end = 0;
-            nf = 0;
-            delta = 0;
+            nf_u = 0;
+            delta_u = 0;
             s = ps;
         } else if (ps != s) {
             flush_start();
             s = ps;
         }
+        if (Lg.chi && u == Lg.u1 - 1) reach = max(reach, (uint32_t)e);
         const int p = P.p;
-        const int t = dtype[p];
-        if (!ven[v * T + t]) return;
+        const int t = Tb.dtype[p];
+        if (!Tb.ven[v * T + t]) return;
         int prev_end = -1;
         if (spilled) {
-            prev_end = (int)cur_s[p];
+            for (uint32_t q = 0; q < n_spill; ++q)
+                if ((int)spill[q].x == p) prev_end = (int)spill[q].y;
         } else {
 #pragma unroll
             for (int q = 0; q < LIVE; ++q)
@@ -1137,7 +1387,10 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
         }
         if (s < prev_end) return;               // inside p's previous match (finditer)
         if (spilled) {
-            cur_s[p] = (uint32_t)e;
+            uint32_t q = 0;
+            while (q < n_spill && (int)spill[q].x != p) ++q;
+            spill[q] = make_uint2((uint32_t)p, (uint32_t)e);
+            if (q == n_spill) ++n_spill;
         } else {
             int slot = -1;
 #pragma unroll
@@ -1155,16 +1408,16 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
                         lp[q] = p;
                         le[q] = e;
                     }
-            } else {
-                for (int q = 0; q < R.P; ++q) cur_s[q] = 0;
+            } else {                             // more than LIVE patterns live: list in global memory
+                n_spill = 0;
 #pragma unroll
                 for (int q = 0; q < LIVE; ++q)
-                    if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
-                cur_s[p] = (uint32_t)e;
+                    if (lp[q] >= 0) spill[n_spill++] = make_uint2((uint32_t)lp[q], (uint32_t)le[q]);
+                spill[n_spill++] = make_uint2((uint32_t)p, (uint32_t)e);
                 spilled = true;
             }
         }
-        const int xi = dex[p];
+        const int xi = Tb.dex[p];
         const int lik = P.lik;
         if (lik < minlik) {                        // invalid (-1) or below min_likelihood
             if (xi != 0xff) ex_valid &= ~(1u << xi);
@@ -1180,10 +1433,10 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
                 }
             ex_valid |= 1u << xi;
         }
-        const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
+        const uint32_t x0 = Tb.xoff[v * T + t], x1 = Tb.xoff[v * T + t + 1];
         bool excluded = false;
         for (uint32_t q = x0; q < x1; ++q) {
-            const int xt = xids[q];
+            const int xt = Tb.xids[q];
 #pragma unroll
             for (int x = 0; x < NE_MAX; ++x)
                 if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
@@ -1198,36 +1451,179 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
             best_lik = lik;
         }
     };
-    // pend[] (4 B per pair, the lane's run at pend + lane_pair[c]) is read 16 entries per iteration as
-    // four aligned 16-byte loads, the next group issued before this one is decoded; only matched pairs
-    // (e >= 0, a small fraction) enter the body.  pend is allocated 16 entries past pair_cap, so the
-    // aligned groups never leave the allocation; entries outside the lane's run are masked off.
-    const uint64_t pbase = lane_pair[c];
-    const uint32_t off0 = (uint32_t)(pbase & 3u);
-    const int4* pa = reinterpret_cast<const int4*>(pend + (pbase - off0));
-    const uint32_t ng = (off0 + np + 15u) >> 4;
-    int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
-    for (uint32_t g = 0; g < ng; ++g) {
-        const int4 c0 = q0, c1 = q1, c2 = q2, c3 = q3;
-        if (g + 1 < ng) {
-            const int4* pn = pa + 4 * (g + 1);
-            q0 = pn[0];
-            q1 = pn[1];
-            q2 = pn[2];
-            q3 = pn[3];
+    for (lane = c0; lane <= c1; ++lane) {
+        Lg = g_lane(g, lane);
+        fdl = io.fd + fd_base(Lg, lane, R.min_len);
+        nfl = 0;
+        rdx = rdy = 0;
+        reach = 0;
+        const uint32_t np = io.lane_np[lane];
+        const uint64_t pbase = io.lane_pair[lane];
+        if (np && pbase + np <= io.pair_cap) {
+            // pend[] (4 B per pair, the lane's run) is read 16 entries per iteration as four aligned
+            // 16-byte loads, the next group issued before this one is decoded; only matched pairs
+            // (e >= 0, a small fraction) enter the body.  pend is allocated 16 entries past pair_cap,
+            // so the aligned groups never leave the allocation; entries outside the run are masked off.
+            const int32_t* el = io.pend + pbase;
+            const uint32_t off0 = (uint32_t)(pbase & 3u);
+            const int4* pa = reinterpret_cast<const int4*>(io.pend + (pbase - off0));
+            const uint32_t ng = (off0 + np + 15u) >> 4;
+            int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
+            for (uint32_t gi = 0; gi < ng; ++gi) {
+                const int4 d0 = q0, d1 = q1, d2 = q2, d3 = q3;
+                if (gi + 1 < ng) {
+                    const int4* pn = pa + 4 * (gi + 1);
+                    q0 = pn[0];
+                    q1 = pn[1];
+                    q2 = pn[2];
+                    q3 = pn[3];
+                }
+                const uint32_t g0 = 16u * gi;
+                uint32_t m = matched_mask16(d0, d1, d2, d3, g0, off0, np);
+                while (m) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    const uint32_t i = g0 + j - off0;
+                    pair(pbase + i, el[i]);      // (the entry is in L1: its group was just loaded)
+                }
+            }
         }
-        const uint32_t g0 = 16u * g;
-        uint32_t m = matched_mask16(c0, c1, c2, c3, g0, off0, np);
-        while (m) {
-            const uint32_t j = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            const uint32_t i = g0 + j - off0;
-            pair(i, el[i]);        // (the entry is in L1: its group was just loaded)
+        // the pending start and (unless the row continues into the next lane) the utterance end here
+        if (u != 0xffffffffu) {
+            flush_start();
+            if (!(Lg.chi && u == Lg.u1 - 1)) {
+                flush_utt();
+                u = 0xffffffffu;
+            }
+        }
+        io.lane_nf[lane] = nfl;
+        io.lane_rd[lane] = make_int2(rdx, rdy);
+        if (Lg.chi) io.lane_reach[lane] = reach;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
+                                                const Geo g, const SelIO io, const uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    if (*err & ERR_QUEUE) return;           // the batch is re-run with a larger queue
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const SelTabs Tb = sel_tabs(lb, li);
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= g.n_chunks) return;
+    select_run(R, Tb, g, io, c, c);
+}
+
+// ---- cut rows: which continuation lanes need the carried state (a match of an earlier lane of the
+// row reaches past their first start), one workgroup per long row.  dirty[c] is written for every
+// lane of the row (0 for the lane holding the row start unless it continues another cut row).
+constexpr int ROW_BLOCK = 1024;
+
+// inclusive max / sum scans over a row's lanes, ROW_BLOCK x 4 per round
+__device__ __forceinline__ uint32_t block_incl_max(uint32_t x, uint32_t* sh) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(x, d);
+        if (lane >= d) x = max(x, o);
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int w = 0; w < wid; ++w) pre = max(pre, sh[w]);
+    __syncthreads();
+    return max(x, pre);
+}
+
+__global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint32_t* __restrict__ long_rows,
+                                                        const uint32_t* __restrict__ long_count,
+                                                        const uint32_t* __restrict__ lane_reach,
+                                                        uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
+    __shared__ uint32_t sh[ROW_BLOCK / 64];
+    __shared__ uint32_t s_carry;
+    if (*err & ERR_QUEUE) return;
+    for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
+        uint32_t ca, kb;
+        int64_t s_r, e_r;
+        row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
+        if (threadIdx.x == 0) {
+            s_carry = 0;
+            if (!g_cut(g, ca)) dirty[ca] = 0;
+        }
+        __syncthreads();
+        // dirty[c] (c in (ca, kb]) = max(reach over lanes [ca, c)) > first start of c (row relative)
+        for (uint32_t c0 = ca; c0 < kb; c0 += ROW_BLOCK) {
+            const uint32_t j = c0 + threadIdx.x;        // lane j's reach feeds dirty[j + 1]
+            const uint32_t x = j < kb ? lane_reach[j] : 0u;
+            const uint32_t incl = max(block_incl_max(x, sh), s_carry);
+            if (j < kb) {
+                const int64_t first = g_cpos(g, j + 1) + 1 - s_r;
+                dirty[j + 1] = (int64_t)incl > first ? 1 : 0;
+            }
+            __syncthreads();
+            if (threadIdx.x == ROW_BLOCK - 1) s_carry = incl;
+            __syncthreads();
         }
     }
-    if (u != 0xffffffffu) {
-        flush_start();
-        flush_utt();
+}
+
+// re-run every maximal chain of dirty lanes from the clean lane before it (one thread per chain)
+__global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
+                                                 const Geo g, const SelIO io, const uint32_t* __restrict__ long_rows,
+                                                 const uint32_t* __restrict__ long_count,
+                                                 const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
+    if (*err & ERR_QUEUE) return;
+    const uint8_t* lb = load_image(img, li.total, lds4);
+    const SelTabs Tb = sel_tabs(lb, li);
+    for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
+        uint32_t ca, kb;
+        int64_t s_r, e_r;
+        row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
+        for (uint32_t j = ca + threadIdx.x; j < kb; j += blockDim.x) {
+            if (dirty[j] || !dirty[j + 1]) continue;
+            uint32_t c = j + 1;
+            while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
+            select_run(R, Tb, g, io, j, c);
+        }
+    }
+}
+
+// a cut row's output length (its lanes' deltas) and, per continuation lane, the delta of the row's
+// findings in the lanes before it (k_spans places the row's findings in the output with it)
+__global__ __launch_bounds__(ROW_BLOCK) void k_rowlen(const Geo g, const uint32_t* __restrict__ long_rows,
+                                                     const uint32_t* __restrict__ long_count,
+                                                     const int2* __restrict__ lane_rd, int32_t* __restrict__ lane_rowbase,
+                                                     uint32_t* __restrict__ out_len, const uint32_t* __restrict__ err) {
+    __shared__ int32_t sh[ROW_BLOCK / 64];
+    __shared__ int32_t s_carry;
+    if (*err & ERR_QUEUE) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
+        const uint32_t r = long_rows[ri];
+        uint32_t ca, kb;
+        int64_t s_r, e_r;
+        row_lanes(g, r, ca, kb, s_r, e_r);
+        if (threadIdx.x == 0) s_carry = 0;
+        __syncthreads();
+        for (uint32_t c0 = ca; c0 <= kb; c0 += ROW_BLOCK) {
+            const uint32_t c = c0 + threadIdx.x;
+            int32_t x = 0;
+            if (c <= kb) x = c == ca ? lane_rd[c].y : lane_rd[c].x;
+            int32_t incl = x;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int32_t o = __shfl_up(incl, d);
+                if (lane >= d) incl += o;
+            }
+            if (lane == 63) sh[wid] = incl;
+            __syncthreads();
+            int32_t pre = s_carry;
+            for (int w = 0; w < wid; ++w) pre += sh[w];
+            if (c <= kb && c > ca) lane_rowbase[c] = pre + incl - x;
+            __syncthreads();
+            if (threadIdx.x == ROW_BLOCK - 1) s_carry = pre + incl;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out_len[r] = (uint32_t)((e_r - s_r) + s_carry);
+        __syncthreads();
     }
 }
 
@@ -1436,10 +1832,10 @@ __global__ __launch_bounds__(LB_BLOCK) void k_scan_lb(const uint32_t* __restrict
 }
 
 __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t* __restrict__ span_offs,
-                           uint32_t n_utt, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
+                           uint32_t n_utt, uint32_t n_span_rows, uint64_t out_cap, uint64_t span_cap, uint32_t* __restrict__ err,
                            uint64_t* __restrict__ totals, const unsigned long long* __restrict__ pair_count,
                            const uint64_t* __restrict__ ev_count, const uint64_t* __restrict__ wf_count) {
-    const uint64_t ob = out_offs[n_utt], ns = span_offs[n_utt];
+    const uint64_t ob = out_offs[n_utt], ns = span_offs[n_span_rows];
     if (ob > out_cap || ns > span_cap) atomicOr(err, (uint32_t)ERR_CAPACITY);
     totals[0] = ob;
     totals[1] = ns;
@@ -1450,37 +1846,28 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
 }
 
 // ---------------------------------------------------------------------------------- k_redact
-// Prefix-sum scatter.  A workgroup owns REDACT_UTT consecutive utterances: one contiguous input range
-// and one contiguous output range.  It builds a PIECE table in LDS (copy runs and "[INFO_TYPE]"
-// tokens, sorted by output offset; 1 + 2*findings pieces per utterance) and copies the spans, then
-// a block -> piece table (each piece marks the first output block it can start, a prefix max fills
-// the rest).  Lane i assembles aligned 16-byte OUTPUT blocks i, i+256, ... so every load and store
-// instruction of a wavefront covers 1 KiB of consecutive bytes: a block inside one piece is two
-// aligned 16-byte source loads + a funnel shift (v_alignbyte), a block that straddles pieces ORs the
-// masked windows of each piece it touches.  Source bytes never pass through LDS.  Only the two
-// partial blocks at a tile's output edges use byte stores.  Tiles with more pieces than fit fall
-// back to a wavefront-per-utterance byte copy; tiles with more output blocks than the block table
-// holds look pieces up by binary search.
+// Span-driven scatter.  Utterance boundaries do not matter to the copy: the output is the batch's
+// bytes with every kept span replaced by its "[INFO_TYPE]" token, i.e. long copy runs (~1 KiB apart at
+// config 2) and short tokens.  k_spans lists every span with its input range and output position
+// (RSpan, in batch order); a workgroup then owns one 64 KiB tile of the OUTPUT (address-aligned),
+// finds its first span (k_tile_first), builds the tile's PIECE table in LDS (copy runs and tokens)
+// and a block -> piece table, and lane i assembles aligned 16-byte output blocks i, i+256, ... so
+// every load and store instruction of a wavefront covers 1 KiB of consecutive bytes: a block inside
+// one piece is two aligned 16-byte source loads + a funnel shift (v_alignbyte), a block that
+// straddles pieces ORs the masked windows of each piece it touches.  Source bytes never pass through
+// LDS.  A tile with more spans than the piece table holds is assembled in several passes.  Rows of
+// any length (a whole transcript) take the same path.
 constexpr int REDACT_BLOCK = 256;
-constexpr int REDACT_UTT = 256;     // utterances per workgroup
 constexpr int PIECE_MAX = 1024;
 constexpr int BLK_MAX = 4096;       // output blocks (64 KiB) covered by the block -> piece table
+constexpr uint32_t RTILE_SHIFT = 16;  // output tile: 64 KiB = BLK_MAX blocks
+constexpr int SPAN_PASS = 500;      // spans per assembly pass (2 pieces each + 2 <= PIECE_MAX)
 
-__device__ uint32_t redact_byte_slow(const RulesDev& R, const uint8_t* src, const pii_span* fdu, uint32_t nf,
-                                     uint32_t rel) {
-    uint32_t pin = 0, pout = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
-        const pii_span F = fdu[f];
-        const uint32_t run = F.start - pin;
-        if (rel < pout + run) return src[pin + (rel - pout)];
-        pout += run;
-        const uint32_t t0 = R.tok_off[F.info_type], tl = R.tok_off[F.info_type + 1] - t0;
-        if (rel < pout + tl) return R.tok_bytes[t0 + (rel - pout)];
-        pout += tl;
-        pin = F.end;
-    }
-    return src[pin + (rel - pout)];
-}
+struct RSpan {          // one kept span in batch order (16 B)
+    uint64_t out;       // output position of its token | info type << 48
+    uint32_t in_lo;     // input range [in_lo, in_hi), batch relative
+    uint32_t in_hi;
+};
 
 // Output assembly shared by k_redact and k_win_redact.  The piece table (s_pout = tile-relative
 // output offset of each piece, s_psrc = ABSOLUTE device address of its first byte; a sentinel
@@ -1584,110 +1971,150 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
     }
 }
 
+// Per lane: its findings -> the API span list (pii_span at lane_sp[c] + k, batch order = (utterance,
+// start) order) and the RSpan list; per-workgroup per-type histogram partials.  A finding's output
+// position = its utterance's output offset + its start + the deltas of the utterance's earlier
+// findings (for a cut row, starting from lane_rowbase: the row's findings in earlier lanes).
+__global__ __launch_bounds__(256) void k_spans(const RulesDev R, const Geo g, const pii_span* __restrict__ fd,
+                                               const uint32_t* __restrict__ lane_nf,
+                                               const uint64_t* __restrict__ lane_sp,
+                                               const int32_t* __restrict__ lane_rowbase,
+                                               const uint64_t* __restrict__ out_offs, const uint32_t* __restrict__ err,
+                                               pii_span* __restrict__ spans, RSpan* __restrict__ rsp,
+                                               uint32_t* __restrict__ hist_part, uint32_t hist_types) {
+    __shared__ uint32_t sh_hist[1024];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool run = *err == 0;
+    for (uint32_t i = threadIdx.x; i < hist_types; i += blockDim.x) sh_hist[i] = 0;
+    __syncthreads();
+    const uint32_t nf = run && c < g.n_chunks ? lane_nf[c] : 0u;
+    if (nf) {
+        const Lane L = g_lane(g, c);
+        const pii_span* f0 = fd + fd_base(L, c, R.min_len);
+        const uint64_t sp0 = lane_sp[c];
+        uint32_t u = 0xffffffffu;
+        int64_t running = 0, ubase_in = 0, ubase_out = 0;
+        for (uint32_t k = 0; k < nf; ++k) {
+            const pii_span F = f0[k];
+            if (F.utt != u) {
+                u = F.utt;
+                running = (L.clo && u == L.u0) ? lane_rowbase[c] : 0;
+                ubase_in = g_off(g, u);
+                ubase_out = (int64_t)out_offs[u];
+            }
+            spans[sp0 + k] = F;
+            const uint32_t t = F.info_type;
+            const int64_t tl = (int64_t)(R.tok_off[t + 1] - R.tok_off[t]);
+            RSpan rs;
+            rs.in_lo = (uint32_t)(ubase_in + F.start);
+            rs.in_hi = (uint32_t)(ubase_in + F.end);
+            rs.out = (uint64_t)(ubase_out + F.start + running) | ((uint64_t)t << 48);
+            rsp[sp0 + k] = rs;
+            running += tl - (int64_t)(F.end - F.start);
+            if (t < hist_types) atomicAdd(&sh_hist[t], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < hist_types; i += blockDim.x)
+        hist_part[(size_t)i * gridDim.x + blockIdx.x] = sh_hist[i];
+}
+
+__device__ __forceinline__ uint64_t rs_out(const RSpan& r) { return r.out & 0xffffffffffffull; }
+__device__ __forceinline__ uint32_t rs_type(const RSpan& r) { return (uint32_t)(r.out >> 48); }
+
+// first span whose token ends after the tile's first output byte (binary search, one thread per tile)
+__global__ __launch_bounds__(256) void k_tile_first(const RulesDev R, const RSpan* __restrict__ rsp,
+                                                    const uint64_t* __restrict__ n_spans_p,
+                                                    const uint64_t* __restrict__ out_total_p, uint32_t omis,
+                                                    uint32_t max_tiles, const uint32_t* __restrict__ err,
+                                                    uint32_t* __restrict__ tile_first) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= max_tiles || *err) return;
+    const int64_t lo = ((int64_t)k << RTILE_SHIFT) - omis;
+    if (lo >= (int64_t)*out_total_p) return;
+    uint64_t a = 0, b = *n_spans_p;          // first i in [a, b) with token end > lo
+    while (a < b) {
+        const uint64_t m = (a + b) >> 1;
+        const RSpan r = rsp[m];
+        const uint32_t t = rs_type(r);
+        if ((int64_t)(rs_out(r) + (R.tok_off[t + 1] - R.tok_off[t])) > lo) b = m;
+        else a = m + 1;
+    }
+    tile_first[k] = (uint32_t)a;
+}
+
 __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const uint8_t* __restrict__ text,
-                                                         const uint64_t* __restrict__ offs, uint32_t n_utt,
-                                                         const pii_span* __restrict__ fd,
-                                                         const uint32_t* __restrict__ n_find,
-                                                         const uint64_t* __restrict__ out_offs,
-                                                         const uint64_t* __restrict__ span_offs,
-                                                         const uint32_t* __restrict__ err, uint8_t* __restrict__ out,
-                                                         pii_span* __restrict__ spans,
-                                                         uint32_t* __restrict__ hist_part) {
-    __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (tile relative)
+                                                         const uint64_t* __restrict__ offs,
+                                                         const RSpan* __restrict__ rsp,
+                                                         const uint64_t* __restrict__ n_spans_p,
+                                                         const uint64_t* __restrict__ out_total_p, uint64_t in_total,
+                                                         const uint32_t* __restrict__ tile_first,
+                                                         const uint32_t* __restrict__ err, uint8_t* __restrict__ out) {
+    __shared__ uint32_t s_pout[PIECE_MAX + 1];     // piece output offset (pass relative)
     __shared__ uint64_t s_psrc[PIECE_MAX + 1];     // piece source address (text or token table)
     __shared__ uint32_t s_wsum[REDACT_BLOCK / 64];
     __shared__ uint16_t s_bp[BLK_MAX];             // output block -> piece holding its first byte
-    __shared__ uint32_t sh_hist[256];
     if (*err != 0) return;
-    const uint32_t u0 = blockIdx.x * REDACT_UTT;
-    const uint32_t u1 = min(u0 + REDACT_UTT, n_utt);
-    const uint32_t nu = u1 - u0;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = tid; i < 256; i += REDACT_BLOCK) sh_hist[i] = 0;
-    const uint64_t base = offs[0];
-    const int64_t out_lo = (int64_t)out_offs[u0], out_hi = (int64_t)out_offs[u1];
-    // ---- per utterance: piece count, block scan ----
-    const bool mine = (uint32_t)tid < nu;
-    const uint32_t u = u0 + tid;
-    uint32_t nf = 0;
-    uint64_t s_abs = 0, o_abs = 0, sp_off = 0;
-    if (mine) {
-        nf = n_find[u];
-        s_abs = offs[u];
-        o_abs = out_offs[u];
-        sp_off = span_offs[u];
-    }
-    const uint32_t cnt = mine ? 1 + 2 * nf : 0;
-    uint32_t incl = cnt;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d);
-        if (lane >= d) incl += o;
-    }
-    if (lane == 63) s_wsum[wid] = incl;
-    __syncthreads();
-    uint32_t wpre = 0, total_p = 0;
-    for (int w = 0; w < REDACT_BLOCK / 64; ++w) {
-        if (w < wid) wpre += s_wsum[w];
-        total_p += s_wsum[w];
-    }
-    const bool staged = total_p <= PIECE_MAX;
-    // ---- piece table + spans + histogram ----
-    if (mine) {
-        uint32_t pb = wpre + incl - cnt;
-        uint32_t po = (uint32_t)((int64_t)o_abs - out_lo);
-        const uint64_t src0 = (uint64_t)(uintptr_t)(text + s_abs);
-        if (nf == 0) {
-            if (staged) {
-                s_pout[pb] = po;
-                s_psrc[pb] = src0;
+    const int64_t out_total = (int64_t)*out_total_p;
+    const uint64_t n_spans = *n_spans_p;
+    const int64_t omis = (int64_t)((uintptr_t)out & 15);
+    const int64_t t_lo = max<int64_t>(((int64_t)blockIdx.x << RTILE_SHIFT) - omis, 0);
+    const int64_t t_hi = min<int64_t>(((int64_t)(blockIdx.x + 1) << RTILE_SHIFT) - omis, out_total);
+    if (t_lo >= t_hi) return;
+    const uint8_t* tb = text + offs[0];
+    const int k = threadIdx.x;
+    uint64_t i = tile_first[blockIdx.x];          // first span whose token ends after t_lo
+    int64_t lo = t_lo;
+    while (lo < t_hi) {
+        // one pass: spans i .. i + n - 1 (their tokens start before the tile end; n <= SPAN_PASS);
+        // piece 2k = the copy run before span i + k, 2k + 1 = its token, 2n = the run after the last
+        const uint64_t j = i + (uint64_t)k;
+        RSpan r{0, 0, 0};
+        bool mine = false;
+        if (k < SPAN_PASS && j < n_spans) {
+            r = rsp[j];
+            mine = (int64_t)rs_out(r) < t_hi;
+        }
+        const uint32_t n = (uint32_t)__syncthreads_count(mine);
+        int64_t hi = t_hi;                            // a full pass ends where the next token starts
+        if (n == (uint32_t)SPAN_PASS && i + n < n_spans) hi = min<int64_t>(hi, (int64_t)rs_out(rsp[i + n]));
+        if (mine) {
+            const uint32_t ty = rs_type(r);
+            const int64_t so = (int64_t)rs_out(r);
+            const int64_t tl = (int64_t)(R.tok_off[ty + 1] - R.tok_off[ty]);
+            if (k == 0) {                             // from lo, shifted like the run before span i
+                s_pout[0] = 0;
+                s_psrc[0] = (uint64_t)(uintptr_t)(tb + (lo - (so - (int64_t)r.in_lo)));
+            } else {                                  // from the previous token's end
+                const RSpan pr = rsp[j - 1];
+                const uint32_t pt = rs_type(pr);
+                const int64_t pe = (int64_t)rs_out(pr) + (int64_t)(R.tok_off[pt + 1] - R.tok_off[pt]);
+                s_pout[2 * k] = (uint32_t)(pe - lo);
+                s_psrc[2 * k] = (uint64_t)(uintptr_t)(tb + pr.in_hi);
             }
-        } else {
-            const pii_span* fdu = fd + (s_abs - base) / (uint64_t)R.min_len;
-            pii_span* sp = spans + sp_off;
-            uint32_t pin = 0;
-            for (uint32_t f = 0; f < nf; ++f) {
-                const pii_span F = fdu[f];
-                sp[f] = F;
-                if (F.info_type < 256) atomicAdd(&sh_hist[F.info_type], 1u);
-                const uint32_t t0 = R.tok_off[F.info_type];
-                if (staged) {
-                    s_pout[pb] = po;
-                    s_psrc[pb] = src0 + pin;
-                    po += F.start - pin;
-                    ++pb;
-                    s_pout[pb] = po;
-                    s_psrc[pb] = (uint64_t)(uintptr_t)(R.tok_bytes + t0);
-                    po += R.tok_off[F.info_type + 1] - t0;
-                    ++pb;
-                }
-                pin = F.end;
-            }
-            if (staged) {
-                s_pout[pb] = po;
-                s_psrc[pb] = src0 + pin;
+            const int64_t ts = max(so, lo);
+            s_pout[2 * k + 1] = (uint32_t)(ts - lo);
+            s_psrc[2 * k + 1] = (uint64_t)(uintptr_t)(R.tok_bytes + R.tok_off[ty] + (ts - so));
+            if ((uint32_t)k + 1 == n) {
+                const int64_t te = min(so + tl, hi);
+                s_pout[2 * n] = (uint32_t)(te - lo);
+                s_psrc[2 * n] = (uint64_t)(uintptr_t)(tb + r.in_hi);
+                s_pout[2 * n + 1] = (uint32_t)(hi - lo);           // sentinel
             }
         }
-    }
-    if (tid == 0 && staged) s_pout[total_p] = (uint32_t)(out_hi - out_lo);   // sentinel
-    __syncthreads();
-    if (staged) {
-        tile_assemble(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
-    } else {
-        // too many pieces: one wavefront per utterance, byte-granular
-        for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
-            const uint32_t uu = u0 + i;
-            const uint64_t sa = offs[uu];
-            const uint8_t* src = text + sa;
-            const uint32_t nfu = n_find[uu];
-            const pii_span* fdu = fd + (sa - base) / (uint64_t)R.min_len;
-            uint8_t* dst = out + out_offs[uu];
-            const uint32_t olen = (uint32_t)(out_offs[uu + 1] - out_offs[uu]);
-            for (uint32_t rel = lane; rel < olen; rel += 64)
-                dst[rel] = (uint8_t)(nfu ? redact_byte_slow(R, src, fdu, nfu, rel) : src[rel]);
+        if (n == 0 && k == 0) {                       // no token in [lo, hi): one copy run
+            const int64_t shift = i < n_spans ? (int64_t)rs_out(rsp[i]) - (int64_t)rsp[i].in_lo
+                                              : out_total - (int64_t)in_total;
+            s_pout[0] = 0;
+            s_psrc[0] = (uint64_t)(uintptr_t)(tb + (lo - shift));
+            s_pout[1] = (uint32_t)(hi - lo);
         }
+        __syncthreads();
+        tile_assemble(s_pout, s_psrc, n == 0 ? 1u : 2 * n + 1, s_bp, s_wsum, out, lo, hi);
+        __syncthreads();
+        i += n;
+        lo = hi;
     }
-    __syncthreads();
-    for (int i = tid; i < R.T && i < 256; i += REDACT_BLOCK) hist_part[(size_t)i * gridDim.x + blockIdx.x] = sh_hist[i];
 }
 
 // per-info-type totals of the redact tiles' histograms (one atomic per type, no same-address storms)
@@ -2605,6 +3032,7 @@ struct pii_engine {
         const uint8_t* text;
         const uint64_t* offs;
         uint32_t n_utt;
+        uint64_t base;
         uint64_t total;
         const uint32_t* slot;
         const uint8_t* role;
@@ -2617,7 +3045,8 @@ struct pii_engine {
         int16_t* ctx_info;
         hipStream_t st;
     } last{};
-    int16_t *kw = nullptr, *ctx = nullptr;
+    int32_t* kw = nullptr;
+    int16_t* ctx = nullptr;
     int32_t *agg_v = nullptr, *commit = nullptr;
     uint64_t *span_offs = nullptr, *bsum = nullptr, *out_offs_tmp = nullptr;
     unsigned long long *lb_state = nullptr, *lb_ticket = nullptr;   // single-pass scan tiles / ticket counter
@@ -2656,6 +3085,24 @@ struct pii_engine {
     uint32_t wcap_utt = 0;
     pii_span* wfd = nullptr;
     uint64_t wfd_cap = 0;
+    // lane-based resolve, long rows, span-driven redaction
+    uint32_t r0 = 0, long_min = NO_CUTS;
+    uint32_t* long_rows = nullptr;     // rows cut into several lanes (k_chunk_index)
+    uint32_t* long_count = nullptr;
+    uint64_t cap_long = 0, cap_ev = 0, cap_fd = 0;
+    uint32_t* lane_st = nullptr;       // [2 * lanes] scan state handed across cuts (k_scan_fix)
+    uint32_t* lane_nf = nullptr;       // findings per lane
+    int2* lane_rd = nullptr;           // cut-row deltas per lane
+    uint32_t* lane_reach = nullptr;
+    int32_t* lane_rowbase = nullptr;
+    uint8_t* dirty = nullptr;
+    uint64_t* lane_sp = nullptr;       // exclusive scan of lane_nf (span offsets); [lanes] = total spans
+    uint2* spill = nullptr;            // k_select's per-run (pattern, end) lists, indexed like the pair queue
+    RSpan* rsp = nullptr;
+    uint64_t cap_rsp = 0;
+    uint32_t* tile_first = nullptr;
+    uint64_t cap_tiles = 0;
+    uint32_t hist_types = 0;           // types counted per workgroup in LDS (k_spans)
 };
 
 #define HIPCHK(x)                                                                  \
@@ -2688,20 +3135,27 @@ int grow_pairs(pii_engine* e, uint64_t cap) {
     }
     int rc;
     if ((rc = grow(e, e->pres, cap)) || (rc = grow(e, e->pend, cap + 16)) || (rc = grow(e, e->matched, cap)) ||
-        (rc = grow(e, e->cont, cap)))
+        (rc = grow(e, e->cont, cap)) || (rc = grow(e, e->spill, cap + 16)))
         return rc;
     return PII_OK;
 }
 
 int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lanes) {
     int rc = PII_OK;
-
-    if (bytes > e->cap_bytes) {
-        const uint64_t nb = std::max<uint64_t>(bytes + bytes / 8, 1 << 16);
-        if ((rc = grow(e, e->ev, nb + 1))) return rc;
-        if ((rc = grow(e, e->fd, nb / e->R.min_len + 2))) return rc;
-        e->cap_bytes = nb;
+    // event arenas: a lane's emitted positions + its utterance starts (ev_base); findings arenas:
+    // one finding per min_len bytes + one per lane (fd_base)
+    const uint64_t need_ev = bytes + n_utt + n_lanes + 2, need_fd = bytes / e->R.min_len + n_lanes + 2;
+    if (need_ev > e->cap_ev) {
+        const uint64_t nb = std::max<uint64_t>(need_ev + need_ev / 8, 1 << 16);
+        if ((rc = grow(e, e->ev, nb))) return rc;
+        e->cap_ev = nb;
     }
+    if (need_fd > e->cap_fd) {
+        const uint64_t nb = std::max<uint64_t>(need_fd + need_fd / 8, 1 << 12);
+        if ((rc = grow(e, e->fd, nb))) return rc;
+        e->cap_fd = nb;
+    }
+    if (bytes > e->cap_bytes) e->cap_bytes = bytes;
     if (n_lanes + 2 > e->cap_lanes) {
         const uint64_t nl = std::max<uint64_t>(n_lanes + n_lanes / 8 + 2, 1024);
         if ((rc = grow(e, e->first_utt, nl))) return rc;
@@ -2713,13 +3167,25 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         if ((rc = grow(e, e->bnd, nl * LANE_WORDS))) return rc;
         if ((rc = grow(e, e->lane_pair, nl))) return rc;
         if ((rc = grow(e, e->lane_np, nl))) return rc;
+        if ((rc = grow(e, e->lane_st, 2 * nl))) return rc;
+        if ((rc = grow(e, e->lane_nf, nl))) return rc;
+        if ((rc = grow(e, e->lane_rd, nl))) return rc;
+        if ((rc = grow(e, e->lane_reach, nl))) return rc;
+        if ((rc = grow(e, e->lane_rowbase, nl))) return rc;
+        if ((rc = grow(e, e->dirty, nl))) return rc;
+        if ((rc = grow(e, e->lane_sp, nl + 1))) return rc;
+        if ((rc = grow(e, e->hist_part, (nl / 256 + 2) * (size_t)std::max<uint32_t>(e->hist_types, 1)))) return rc;
         e->cap_lanes = nl;
         e->cap_bsum = 0;
+    }
+    const uint64_t need_long = std::min<uint64_t>((uint64_t)n_utt + 1, bytes / 1024 + 2);
+    if (need_long > e->cap_long) {
+        if ((rc = grow(e, e->long_rows, need_long))) return rc;
+        e->cap_long = need_long;
     }
     if (n_utt > e->cap_utt) {
         const uint32_t nu = std::max<uint32_t>(n_utt + n_utt / 8, 1024);
         if ((rc = grow(e, e->n_ev, nu))) return rc;
-        if ((rc = grow(e, e->n_find, nu))) return rc;
         if ((rc = grow(e, e->out_len, nu))) return rc;
         if ((rc = grow(e, e->incl, nu))) return rc;
         if ((rc = grow(e, e->kw, nu))) return rc;
@@ -2728,9 +3194,6 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         const uint32_t nblk = nu / CTX_BLOCK + 2;
         if ((rc = grow(e, e->agg_v, nblk))) return rc;
         if ((rc = grow(e, e->agg_f, nblk))) return rc;
-        if ((rc = grow(e, e->span_offs, (size_t)nu + 1))) return rc;
-        if ((rc = grow(e, e->out_offs_tmp, (size_t)nu + 1))) return rc;
-        if ((rc = grow(e, e->hist_part, ((size_t)nu / REDACT_UTT + 2) * (size_t)std::max(e->R.T, 1)))) return rc;
         e->cap_utt = nu;
         e->cap_bsum = 0;
     }
@@ -2740,6 +3203,22 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         e->cap_bsum = n;
     }
     return rc;
+}
+
+// span list + output tiles for a call with these capacities
+int ensure_redact(pii_engine* e, uint64_t span_cap, uint64_t out_cap) {
+    int rc;
+    if (span_cap + 1 > e->cap_rsp) {
+        const uint64_t n = std::max<uint64_t>(span_cap + span_cap / 8 + 16, 4096);
+        if ((rc = grow(e, e->rsp, n))) return rc;
+        e->cap_rsp = n;
+    }
+    const uint64_t tiles = (out_cap >> RTILE_SHIFT) + 2;
+    if (tiles > e->cap_tiles) {
+        if ((rc = grow(e, e->tile_first, tiles + tiles / 8))) return rc;
+        e->cap_tiles = tiles + tiles / 8;
+    }
+    return PII_OK;
 }
 
 // Small scans (a re-scan step: ~100k rows) take the single-pass look-back kernel, one launch instead
@@ -2798,42 +3277,71 @@ int ensure_queues(pii_engine* e, uint64_t total_bytes) {
     return PII_OK;
 }
 
-// The stages every call shares: lane index, reverse DFA scan, (start, pattern) pair queue, context
-// (segmented scan), leftmost-first confirmation.  Records tev[0..2].
+// lanes of a batch of `total_bytes` whose base address is r0 mod 64 (slices are address aligned)
+uint32_t lane_count(const pii_engine* e, uint64_t total_bytes) {
+    if (total_bytes == 0) return 0;
+    return (uint32_t)((total_bytes + e->r0 + (1u << e->lane_shift) - 1) >> e->lane_shift);
+}
+
+Geo make_geo(const pii_engine* e, const uint64_t* offs, uint32_t n_utt, uint32_t n_chunks, uint64_t base) {
+    Geo g;
+    g.offs = offs;
+    g.first_utt = e->first_utt;
+    g.base = base;
+    g.n_utt = n_utt;
+    g.n_chunks = n_chunks;
+    g.sh = e->lane_shift;
+    g.r0 = e->r0;
+    g.long_min = e->long_min;
+    return g;
+}
+
+// grid for the per-long-row kernels (they loop over the device-side row list)
+uint32_t row_grid(const pii_engine* e, uint64_t total_bytes) {
+    const uint64_t max_rows = total_bytes / 2048 + 1;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_rows, 2 * (uint64_t)e->n_cu));
+}
+
+// The stages every call shares: lane index, reverse DFA scan (+ the stitching of cut rows), (start,
+// pattern) pair queue, context (segmented scan), leftmost-first confirmation.  Records tev[0..2].
 int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint32_t n_chunks,
-                 const uint32_t* slot, const uint8_t* role, const int64_t* ts, int16_t* ctx, int16_t* win_ctx,
-                 const unsigned long long* pcount, hipStream_t st) {
+                 uint64_t base, uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts,
+                 int16_t* ctx, int16_t* win_ctx, const unsigned long long* pcount, hipStream_t st) {
     const RulesDev& R = e->R;
     e->epoch += 1;
+    const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
     HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), st));
     HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(e->long_count, 0, sizeof(uint32_t), st));
     HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
-        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, R.kw_always_min,
-                                                                e->first_utt, e->out_len, e->n_find, e->kw,
-                                                                win_ctx ? e->wc_n : nullptr);
+        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
+                                                                e->long_min, R.kw_always_min, e->first_utt,
+                                                                e->out_len, e->kw, win_ctx ? e->wc_n : nullptr,
+                                                                e->long_rows, e->long_count);
         if (n_chunks > 0) {
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
-            k_lane_count<<<nsb, 256, 0, st>>>(offs, e->first_utt, n_chunks, e->lane_bkt);
-            k_lane_place<<<nsb, 256, 0, st>>>(offs, e->first_utt, n_chunks, e->lane_bkt,
-                                                                 e->lane_perm, e->lane_pos);
-            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(offs, e->first_utt, n_chunks,
-                                                                (int64_t)((uintptr_t)text & 63), e->lane_pos, e->bnd);
+            k_lane_count<<<nsb, 256, 0, st>>>(g, e->lane_bkt);
+            k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
+            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
             HIPCHK(hipEventRecord(e->kev[0], st));
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
-                R, text, offs, n_utt, e->first_utt, n_chunks, e->bnd, e->lane_perm, e->ev, e->lane_cnt);
+                R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st);
             HIPCHK(hipEventRecord(e->kev[1], st));
+            if (e->long_min != NO_CUTS)
+                k_scan_fix<<<row_grid(e, total_bytes), 256, e->scan_lds, st>>>(R, g, text, e->long_rows, e->long_count,
+                                                                               e->ev, e->lane_cnt, e->lane_st);
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
-            k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
-                                                        e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
-                                                        e->lane_pair, e->lane_ev, e->lane_np, e->d_err);
+            k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc, e->evpairs,
+                                                        e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev, e->lane_np,
+                                                        e->d_err);
             int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
             if ((rc = exclusive_scan(e, e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
-            k_pairs<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, offs, e->first_utt, n_chunks, e->ev, e->lane_cnt, role,
-                                                       e->kw, e->evloc, e->evpairs, e->pair_cap, e->ev_cap,
-                                                       e->lane_pair, e->lane_ev, e->lane_np, e->d_err);
+            k_pairs<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc, e->evpairs,
+                                                       e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev, e->lane_np,
+                                                       e->d_err);
             k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
         }
         HIPCHK(hipGetLastError());
@@ -2858,52 +3366,72 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     return PII_OK;
 }
 
-int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
-                 const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
-                 uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info, hipStream_t st) {
+int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
+                 uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out,
+                 uint64_t out_cap, uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info,
+                 hipStream_t st) {
     if (total_bytes > PII_MAX_BATCH_BYTES) {
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
         return PII_E_ARG;
     }
     e->lane_shift = pick_lane_shift(e, total_bytes);
-    const uint32_t n_chunks = (uint32_t)((total_bytes + (1u << e->lane_shift) - 1) >> e->lane_shift);
+    e->r0 = (uint32_t)(((uintptr_t)text + base) & 63);
+    e->long_min = 2u << e->lane_shift;          // rows longer than two lanes are cut
+    const uint32_t n_chunks = lane_count(e, total_bytes);
     e->last_lanes = n_chunks;
     int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
-    if (rc || (rc = ensure_queues(e, total_bytes))) return rc;
-    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
-                               ctx_info, st};
+    if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_redact(e, span_cap, out_cap))) return rc;
+    e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
+                               span_cap, ctx_info, st};
     e->last_kind = 0;
     const RulesDev& R = e->R;
     int16_t* ctx = ctx_info ? ctx_info : e->ctx;
     e->kev_valid = n_utt > 0 && total_bytes > 0;
+    const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
     // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
     const unsigned long long* pcount =
         n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
-    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, slot, role, ts, ctx, nullptr, pcount, st))) return rc;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, base, total_bytes, slot, role, ts, ctx, nullptr, pcount,
+                           st)))
+        return rc;
     if (n_utt > 0 && n_chunks > 0) {
         k_pair_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
             e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
             e->mcount, e->n_seg, e->evloc, e->pend, e->pres);
-        k_select<<<(n_chunks + 255) / 256, 256, e->img_sel.li.total, st>>>(
-            R, e->img_sel.d, e->img_sel.li, n_chunks, e->lane_pair, e->lane_np, e->evloc, e->pres, e->pend, e->pair_cap, role,
-            ctx, e->fd, e->n_find, e->out_len, e->d_err);
+        const SelIO io{e->lane_pair, e->lane_np, e->evloc, e->pres, e->pend, e->pair_cap, role, ctx, e->fd,
+                       e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill};
+        k_select<<<(n_chunks + 255) / 256, 256, e->img_sel.li.total, st>>>(R, e->img_sel.d, e->img_sel.li, g, io,
+                                                                          e->d_err);
+        const uint32_t rg = row_grid(e, total_bytes);
+        k_sel_dirty<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_reach, e->dirty, e->d_err);
+        k_sel_fix<<<rg, 256, e->img_sel.li.total, st>>>(R, e->img_sel.d, e->img_sel.li, g, io, e->long_rows,
+                                                        e->long_count, e->dirty, e->d_err);
+        k_rowlen<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_rd, e->lane_rowbase, e->out_len,
+                                          e->d_err);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[3], st));
     if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
-    if ((rc = exclusive_scan(e, e->n_find, n_utt, e->span_offs, st))) return rc;
-    k_finalize<<<1, 1, 0, st>>>(out_offs, e->span_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
+    if ((rc = exclusive_scan(e, e->lane_nf, n_chunks, e->lane_sp, st))) return rc;
+    k_finalize<<<1, 1, 0, st>>>(out_offs, e->lane_sp, n_utt, n_chunks, out_cap, span_cap, e->d_err, e->d_totals,
                                 pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
         if (n_chunks > 0) {
-            const uint32_t n_tiles = (n_utt + REDACT_UTT - 1) / REDACT_UTT;
+            const uint32_t nsb = (n_chunks + 255) / 256;
+            k_spans<<<nsb, 256, 0, st>>>(R, g, e->fd, e->lane_nf, e->lane_sp, e->lane_rowbase, out_offs, e->d_err,
+                                         spans, e->rsp, e->hist_part, e->hist_types);
+            const uint32_t tiles = (uint32_t)((out_cap + 15) >> RTILE_SHIFT) + 1;
+            k_tile_first<<<(tiles + 255) / 256, 256, 0, st>>>(R, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
+                                                              (uint32_t)((uintptr_t)out & 15), tiles, e->d_err,
+                                                              e->tile_first);
             HIPCHK(hipEventRecord(e->kev[2], st));
-            k_redact<<<n_tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, n_utt, e->fd, e->n_find, out_offs,
-                                                       e->span_offs, e->d_err, out, spans, e->hist_part);
+            k_redact<<<tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
+                                                     total_bytes, e->tile_first, e->d_err, out);
             HIPCHK(hipEventRecord(e->kev[3], st));
-            k_hist_reduce<<<dim3(std::min(R.T, 256), std::max(1u, std::min(32u, n_tiles / 256))), 256, 0, st>>>(e->hist_part, n_tiles, R.T, e->d_err, e->hist);
+            k_hist_reduce<<<dim3(e->hist_types, std::max(1u, std::min(32u, nsb / 256))), 256, 0, st>>>(
+                e->hist_part, nsb, (int)e->hist_types, e->d_err, e->hist);
         }
         k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
                                                           e->st_group, e->st_ts);
@@ -2940,8 +3468,8 @@ int ensure_window_scratch(pii_engine* e, uint32_t n_utt) {
 
 // the window re-scan call (a12): the shared front over the NEW rows only, then resident candidates,
 // window selection, window redaction, ring commit
-int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
-               const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
+int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
+               uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out, uint64_t out_cap,
                uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* win_ctx, hipStream_t st) {
     if (e->win_n == 0) {
         e->err = "window re-scan not enabled (pii_window_enable)";
@@ -2952,19 +3480,23 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         return PII_E_ARG;
     }
     e->lane_shift = pick_lane_shift(e, total_bytes);
-    const uint32_t n_chunks = (uint32_t)((total_bytes + (1u << e->lane_shift) - 1) >> e->lane_shift);
+    e->r0 = (uint32_t)(((uintptr_t)text + base) & 63);
+    e->long_min = NO_CUTS;                      // the window kernels keep rows whole
+    const uint32_t n_chunks = lane_count(e, total_bytes);
     e->last_lanes = n_chunks;
     int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
     if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_window_scratch(e, n_utt))) return rc;
-    e->last = pii_engine::Call{text, offs, n_utt, total_bytes, slot, role, ts, out, out_cap, out_offs, spans, span_cap,
-                               win_ctx, st};
+    e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
+                               span_cap, win_ctx, st};
     e->last_kind = 1;
     const RulesDev& R = e->R;
     int16_t* wctx = win_ctx ? win_ctx : e->wctx;
     e->kev_valid = n_utt > 0 && total_bytes > 0;
     const unsigned long long* pcount =
         n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
-    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, slot, role, ts, e->ctx, wctx, pcount, st))) return rc;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, base, total_bytes, slot, role, ts, e->ctx, wctx, pcount,
+                           st)))
+        return rc;
     if (n_utt > 0 && n_chunks > 0) {
         k_win_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
             e->img_eval.d, e->img_eval.li, text, offs, pcount, e->pair_cap, e->matched, e->mcount, e->n_seg,
@@ -2990,7 +3522,7 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     if ((rc = exclusive_scan(e, e->wout_len, n_utt, out_offs, st))) return rc;
     if ((rc = exclusive_scan(e, e->n_wfind, n_utt, e->wspan_offs, st))) return rc;
     if (n_utt > 0) k_win_alloc<<<nb, 256, 0, st>>>(W, B, e->wnew, e->d_err);
-    k_finalize<<<1, 1, 0, st>>>(out_offs, e->wspan_offs, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
+    k_finalize<<<1, 1, 0, st>>>(out_offs, e->wspan_offs, n_utt, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
                                 pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, n_utt > 0 ? e->wfbase + n_utt : nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->tev[4], st));
@@ -3013,10 +3545,10 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
 int rerun_last(pii_engine* e) {
     const pii_engine::Call c = e->last;
     if (e->last_kind == 1)
-        return run_window(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
-                          c.spans, c.span_cap, c.ctx_info, c.st);
-    return run_pipeline(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.out, c.out_cap, c.out_offs,
-                        c.spans, c.span_cap, c.ctx_info, c.st);
+        return run_window(e, c.text, c.offs, c.n_utt, c.base, c.total, c.slot, c.role, c.ts, c.out, c.out_cap,
+                          c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st);
+    return run_pipeline(e, c.text, c.offs, c.n_utt, c.base, c.total, c.slot, c.role, c.ts, c.out, c.out_cap,
+                        c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st);
 }
 
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
@@ -3071,7 +3603,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         pii_engine_destroy(e);
         return PII_E_RULES;
     };
-    if (R.P > P_MAX) return fail("more detector patterns than P_MAX");
+    if (R.P > 65535) return fail("too many detector patterns");
     // scan table entries are 16-bit LDS byte addresses (k_scan layout: class map, D rows, K rows);
     // rows are padded to an even class count so every row address is a multiple of 4 and bit 1 of
     // an entry is free for the destination's end-of-text accept
@@ -3287,7 +3819,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("rule tables do not fit in LDS / upload failed");
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first, &e->img_first}, {(const void*)k_pair_eval, &e->img_eval},
-            {(const void*)k_select, &e->img_sel}, {(const void*)k_win_eval, &e->img_eval},
+            {(const void*)k_select, &e->img_sel}, {(const void*)k_sel_fix, &e->img_sel},
+            {(const void*)k_win_eval, &e->img_eval},
             {(const void*)k_win_select, &e->img_wsel}, {(const void*)k_win_halo, &e->img_eval}};
         for (auto& kb : big)
             if (kb.second->li.total > 64 * 1024 &&
@@ -3303,8 +3836,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     if (e->scan_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess)
+        (hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess))
         return fail("cannot raise LDS limit");
+    e->hist_types = (uint32_t)std::min(R.T, 1024);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     e->own_stream = true;
     for (auto& t : e->kev)
@@ -3313,7 +3848,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (hipEventCreate(&t) != hipSuccess) return fail("event");
     const size_t ns = std::max<uint32_t>(1, n_conv_slots);
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
-        hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, 256 * 8) != hipSuccess ||
+        hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, std::max(R.T, 256) * 8) != hipSuccess ||
+        hipMalloc(&e->long_count, 16) != hipSuccess ||
         hipMalloc(&e->d_err, 16) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
         hipMalloc(&e->pair_count, 16) != hipSuccess || hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
         hipMemset(e->lb_ticket, 0, 16) != hipSuccess)
@@ -3322,7 +3858,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     std::vector<int32_t> g(ns, -1);
     if (hipMemcpy(e->st_group, g.data(), ns * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(e->st_ts, 0, ns * 8) != hipSuccess || hipMemset(e->stamp, 0, ns * 4) != hipSuccess ||
-        hipMemset(e->hist, 0, 256 * 8) != hipSuccess)
+        hipMemset(e->hist, 0, std::max(R.T, 256) * 8) != hipSuccess)
         return fail("state init failed");
     k_noop<<<1, 64, 0, e->stream>>>();
     if (hipStreamSynchronize(e->stream) != hipSuccess) return fail("device not usable");
@@ -3339,7 +3875,9 @@ int pii_engine_destroy(pii_engine* e) {
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
-                    e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd};
+                    e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
+                    e->long_rows, e->long_count, e->lane_st, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
+                    e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
@@ -3521,7 +4059,7 @@ int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* 
         HIPCHK(hipMemcpyAsync(e->h_role, role, n_utt, hipMemcpyHostToDevice, st));
         if (ts_us) HIPCHK(hipMemcpyAsync(e->h_ts, ts_us, n_utt * 8, hipMemcpyHostToDevice, st));
     }
-    rc = (window ? run_window : run_pipeline)(e, e->h_text, e->h_offs, n_utt, total, e->h_slot, e->h_role,
+    rc = (window ? run_window : run_pipeline)(e, e->h_text, e->h_offs, n_utt, 0, total, e->h_slot, e->h_role,
                                               ts_us ? e->h_ts : nullptr, e->h_out, out_cap, e->h_out_offs, e->h_spans,
                                               span_cap, e->h_ctx, st);
     if (rc) return rc;
@@ -3553,8 +4091,8 @@ int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64
     HIPCHK(hipMemcpyAsync(tb + 1, d_offsets + n_utt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (tb[1] < tb[0]) return PII_E_ARG;
-    return (window ? run_window : run_pipeline)(e, d_bytes, d_offsets, n_utt, tb[1] - tb[0], d_slot, d_role, d_ts,
-                                                d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx_info, st);
+    return (window ? run_window : run_pipeline)(e, d_bytes, d_offsets, n_utt, tb[0], tb[1] - tb[0], d_slot, d_role,
+                                                d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx_info, st);
 }
 }  // namespace
 
@@ -3572,6 +4110,10 @@ int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
     if (!e || window_n == 0 || window_n > WN_MAX || slot_bytes < 64 || slot_bytes % 16) return PII_E_ARG;
     if (!e->window_ok) {
         e->err = "a detector can match '\\n' or a text edge: windows cannot be re-scanned incrementally";
+        return PII_E_RULES;
+    }
+    if (e->R.P > P_MAX) {
+        e->err = "the window re-scan keeps per-pattern state for at most P_MAX detector patterns";
         return PII_E_RULES;
     }
     HIPCHK(hipSetDevice(e->device));
@@ -3647,16 +4189,17 @@ int pii_histogram(pii_engine* e, uint64_t* counts, uint32_t n) {
     if (!e || !counts) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
-    std::vector<unsigned long long> h(256);
-    HIPCHK(hipMemcpy(h.data(), e->hist, 256 * 8, hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < n; ++i) counts[i] = i < 256 ? h[i] : 0;
+    const uint32_t T = (uint32_t)e->R.T;
+    std::vector<unsigned long long> h(T);
+    if (T) HIPCHK(hipMemcpy(h.data(), e->hist, T * 8, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) counts[i] = i < T ? h[i] : 0;
     return PII_OK;
 }
 
 int pii_histogram_reset(pii_engine* e) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemsetAsync(e->hist, 0, 256 * 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->hist, 0, std::max(e->R.T, 256) * 8, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return PII_OK;
 }
