@@ -49,7 +49,7 @@ constexpr uint32_t MIN_LANE_SHIFT = 7;        // smallest scan lane, 128 B (smal
 constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
-enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16 };
+enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16, ERR_STITCH = 32 };
 
 struct Event {
     uint32_t pos;   // candidate start, relative to the batch base
@@ -588,14 +588,22 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
 }
 
 constexpr int FIX_Q = 512;
+// LDS past the scan tables (the tables' entries are absolute LDS addresses, so the kernel declares no
+// static LDS): queue, entry states, previous round's lanes, counters
+constexpr size_t FIX_LDS = (3 * FIX_Q + 4) * 4;
 
 __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                   const uint32_t* __restrict__ long_rows,
                                                   const uint32_t* __restrict__ long_count, Event* __restrict__ ev,
-                                                  uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st) {
+                                                  uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
+                                                  uint32_t scan_lds, uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
-    __shared__ uint32_t s_q[FIX_Q], s_e[FIX_Q], s_prev[FIX_Q];
-    __shared__ uint32_t s_n, s_np, s_full;
+    uint32_t* s_q = smem32 + scan_lds / 4;
+    uint32_t* s_e = s_q + FIX_Q;
+    uint32_t* s_prev = s_e + FIX_Q;
+    uint32_t& s_n = s_prev[FIX_Q];
+    uint32_t& s_np = s_prev[FIX_Q + 1];
+    uint32_t& s_full = s_prev[FIX_Q + 2];
     const uint32_t nrows = *long_count;
     if (blockIdx.x >= nrows) return;
     {
@@ -613,9 +621,15 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g,
         uint32_t ca, kb;
         int64_t s_r, e_r;
         row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
-        // boundaries c | c + 1 for c in [ca, kb); round 1 checks all of them
+        // boundaries c | c + 1 for c in [ca, kb); round 1 checks all of them.  Every round fixes the
+        // rightmost wrong boundary of each chain, so kb - ca + 1 rounds always suffice (the cap only
+        // guards against a broken invariant: the batch then fails instead of spinning)
         bool all = true;
-        for (;;) {
+        for (uint32_t round = 0;; ++round) {
+            if (round > kb - ca + 1) {
+                if (threadIdx.x == 0) atomicOr(err, (uint32_t)ERR_STITCH);
+                break;
+            }
             if (threadIdx.x == 0) {
                 s_n = 0;
                 s_full = 0;
@@ -1861,7 +1875,7 @@ constexpr int REDACT_BLOCK = 256;
 constexpr int PIECE_MAX = 1024;
 constexpr int BLK_MAX = 4096;       // output blocks (64 KiB) covered by the block -> piece table
 constexpr uint32_t RTILE_SHIFT = 16;  // output tile: 64 KiB = BLK_MAX blocks
-constexpr int SPAN_PASS = 500;      // spans per assembly pass (2 pieces each + 2 <= PIECE_MAX)
+constexpr int SPAN_PASS = REDACT_BLOCK - 1;   // spans per assembly pass: one per thread (2 pieces each + 2 <= PIECE_MAX)
 
 struct RSpan {          // one kept span in batch order (16 B)
     uint64_t out;       // output position of its token | info type << 48
@@ -3330,8 +3344,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st);
             HIPCHK(hipEventRecord(e->kev[1], st));
             if (e->long_min != NO_CUTS)
-                k_scan_fix<<<row_grid(e, total_bytes), 256, e->scan_lds, st>>>(R, g, text, e->long_rows, e->long_count,
-                                                                               e->ev, e->lane_cnt, e->lane_st);
+                k_scan_fix<<<row_grid(e, total_bytes), 256, e->scan_lds + FIX_LDS, st>>>(
+                    R, g, text, e->long_rows, e->long_count, e->ev, e->lane_cnt, e->lane_st, (uint32_t)e->scan_lds,
+                    e->d_err);
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
             k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc, e->evpairs,
                                                         e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev, e->lane_np,
@@ -3836,8 +3851,11 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     if (e->scan_lds > 64 * 1024 &&
-        (hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess ||
-         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess))
+        hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess)
+        return fail("cannot raise LDS limit");
+    if (e->scan_lds + FIX_LDS > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(e->scan_lds + FIX_LDS)) != hipSuccess)
         return fail("cannot raise LDS limit");
     e->hist_types = (uint32_t)std::min(R.T, 1024);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
@@ -3977,6 +3995,10 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
     }
     if (f & ERR_ORDER) return PII_E_ORDER;
     if (f & ERR_QUEUE) return PII_E_NOMEM;
+    if (f & ERR_STITCH) {
+        e->err = "internal: a cut row's lanes did not converge";
+        return PII_E_DEVICE;
+    }
     if (f & ERR_CAPACITY) return PII_E_CAPACITY;
     return PII_OK;
 }
