@@ -208,11 +208,9 @@ __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
 // coalesced.  Blocks past LANE_WORDS use a slow path.
 constexpr int LANE_WORDS = 32;
 
-// exclusive end of the bytes lane L scans: its range, plus a halo past a cut (clamped to the row)
-__device__ __forceinline__ uint32_t scan_top(const Geo& g, const Lane& L) {
-    if (!L.chi) return L.hi;
-    return (uint32_t)min<int64_t>((int64_t)L.hi + SCAN_HALO, g_off(g, L.u1));
-}
+// exclusive end of the bytes lane L scans (a lane cut at hi starts from the state its halo produced,
+// k_lane_bits, instead of stepping the halo itself)
+__device__ __forceinline__ uint32_t scan_top(const Geo& g, const Lane& L) { return L.hi; }
 
 // bits of lane c's i-th block from the top (the slow path for i >= LANE_WORDS: binary search over the
 // lane's utterances; everything is re-derived from (c, i) so the scan keeps nothing live for it)
@@ -222,7 +220,7 @@ __device__ __attribute__((noinline)) uint64_t block_bits_slow(const Geo g, uint3
     const int64_t blk = (((int64_t)top - 1 + g.r0) >> 6) - i;
     const int64_t plo = blk * 64 - g.r0, phi = plo + 64;       // positions [plo, phi)
     uint64_t bits = 0;
-    if ((int64_t)top >= plo && (int64_t)top < phi) bits |= 1ull << (top - plo);
+    if (!L.chi && (int64_t)top >= plo && (int64_t)top < phi) bits |= 1ull << (top - plo);
     const uint32_t vmin = L.u0 + (L.clo ? 1u : 0u);
     if (vmin >= L.u1) return bits;
     // largest v in [vmin, u1) with start < phi
@@ -312,9 +310,41 @@ __global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __res
     }
 }
 
+// table entries are absolute LDS byte addresses of the next row, bit 0 = accept (scan_tables); k_scan
+// has no static LDS, so its dynamic region starts at LDS address 0 and an entry IS the address
+constexpr uint32_t SCAN_TD_BASE = 1024;     // after the 256-entry class map
+typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
+__device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
+    return *reinterpret_cast<lds_u16_t*>((size_t)addr);
+}
+
+// the state a lane carries across a cut: both automata's current rows (flag bits masked off)
+__device__ __forceinline__ uint32_t scan_state(uint32_t nd, uint32_t nk) { return (nd & 0xfffcu) | ((nk & 0xfffcu) << 16); }
+
+// The state a lane cut at hi starts from: both automata stepped right to left over the SCAN_HALO
+// bytes after the cut (clamped to the row) from the start state, tables read from global memory (a
+// cut lane is rare; k_scan_fix verifies the result against the neighbour's real state)
+__device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* __restrict__ text, const Lane& L) {
+    const uint32_t top = (uint32_t)min<int64_t>((int64_t)L.hi + SCAN_HALO, g_off(g, L.u1));
+    const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)(R.SD * R.CDs / 2) * 4;
+    const uint32_t start2 = (uint32_t)R.d_start | ((uint32_t)R.k_start << 16);
+    const uint8_t* tb = text + g.base;
+    uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
+    for (int64_t b = (int64_t)top - 1; b >= (int64_t)L.hi; --b) {
+        const uint32_t x = R.cmap4[tb[b]] + (pm & start2);
+        const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
+        const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
+        nd = R.td[(ad - SCAN_TD_BASE) >> 1];
+        nk = R.tk[(ak - tk_base) >> 1];
+        pm = 0;
+    }
+    return scan_state(nd, nk);
+}
+
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
-__global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* __restrict__ lane_pos,
-                                                   uint64_t* __restrict__ words) {
+__global__ __launch_bounds__(256) void k_lane_bits(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+                                                   const uint32_t* __restrict__ lane_pos,
+                                                   uint64_t* __restrict__ words, uint32_t* __restrict__ lane_st) {
     __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -333,6 +363,7 @@ __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* 
     const Lane L = g_lane(g, c);
     const uint32_t top = scan_top(g, L);
     if (top <= L.lo) return;
+    if (L.chi) lane_st[2 * c] = halo_state(R, g, text, L);
     const int64_t b_hi = ((int64_t)top - 1 + g.r0) >> 6, b_lo = ((int64_t)L.lo + g.r0) >> 6;
     const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
     const uint32_t slot = lane_pos[c];
@@ -342,7 +373,7 @@ __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* 
     for (int64_t i = 0; i < nw; ++i) {
         const int64_t plo = (b_hi - i) * 64 - g.r0;
         uint64_t bits = 0;
-        if (i == 0 && (int64_t)top >= plo && (int64_t)top < plo + 64) bits |= 1ull << (top - plo);
+        if (i == 0 && !L.chi && (int64_t)top >= plo && (int64_t)top < plo + 64) bits |= 1ull << (top - plo);
         while (v >= vmin && sv >= plo) {
             if (sv < plo + 64 && uoff(v + 1) > sv) bits |= 1ull << (sv - plo);
             --v;
@@ -352,24 +383,16 @@ __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* 
     }
 }
 
-// table entries are absolute LDS byte addresses of the next row, bit 0 = accept (scan_tables); k_scan
-// has no static LDS, so its dynamic region starts at LDS address 0 and an entry IS the address
-constexpr uint32_t SCAN_TD_BASE = 1024;     // after the 256-entry class map
-typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
-__device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
-    return *reinterpret_cast<lds_u16_t*>((size_t)addr);
-}
-
-// the lane's events go to its own arena (ev_base): only positions in its emission range [lo_r,
-// lo_r + len_r] are recorded
-__device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t& cnt, uint32_t pos, uint32_t lo_r,
-                                          uint32_t len_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
+// the lane's events go to its own arena (ev + ab, ab = ev_base, 32-bit: the host bounds bytes + rows
+// + lanes of a batch below 2^32): only positions in its emission range [lo_r, lo_r + len_r] are recorded
+__device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t ab, uint32_t& cnt, uint32_t pos,
+                                          uint32_t lo_r, uint32_t len_r, uint32_t ad, uint32_t ak, uint32_t tk_base) {
     if (pos - lo_r <= len_r) {
         Event e;
         e.pos = (uint32_t)pos;
         e.sd = (uint16_t)((ad - SCAN_TD_BASE) >> 1);     // transition index (row * CD + class)
         e.sk = (uint16_t)((ak - tk_base) >> 1);
-        ev[cnt++] = e;
+        ev[(uint64_t)ab + cnt++] = e;
     }
 }
 
@@ -398,7 +421,7 @@ __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t j) {
 // byte j at bit 2 (7 - j): bit 0 = an automaton accepted on the byte (record its transitions ad[j],
 // ak[j], start pos + 1), bit 1 = the byte starts an utterance and the destination row accepts at
 // end of text (record the destination rows' EOT transitions, start pos).
-__device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt, uint32_t m,
+__device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, uint32_t& cnt, uint32_t m,
                                            const uint32_t (&ad)[8], const uint32_t (&ak)[8], uint32_t p0,
                                            uint32_t lo_r, uint32_t len_r, uint32_t tk_base, uint32_t eot_d,
                                            uint32_t eot_k) {
@@ -413,7 +436,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
             k = (lds_u16(k) & 0xfffcu) + eot_k;
             pos -= 1u;
         }
-        scan_emit(ev, cnt, pos, lo_r, len_r, a, k, tk_base);
+        scan_emit(ev, ab, cnt, pos, lo_r, len_r, a, k, tk_base);
     } while (m);
 }
 
@@ -440,7 +463,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
         SCAN_STEP8(7, H) SCAN_STEP8(6, H) SCAN_STEP8(5, H) SCAN_STEP8(4, H)                       \
         SCAN_STEP8(3, H) SCAN_STEP8(2, H) SCAN_STEP8(1, H) SCAN_STEP8(0, H)                       \
         if (__builtin_expect(m != 0, 0))                                                          \
-            scan_emit8(arena, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
+            scan_emit8(ev, ab, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
     }
 
 #define SCAN_SUB(W, OFF)                                                                          \
@@ -450,8 +473,6 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t& cnt
         SCAN_GROUP8(W, 0, OFF)                                                                    \
     }
 
-// the state a lane carries across a cut: both automata's current rows (flag bits masked off)
-__device__ __forceinline__ uint32_t scan_state(uint32_t nd, uint32_t nk) { return (nd & 0xfffcu) | ((nk & 0xfffcu) << 16); }
 
 // Emission range of lane L: event positions [e_lo, e_hi].  A position is reported by the step over the
 // byte before it, so a lane cut at lo leaves position lo to its left neighbour, and a lane cut at hi
@@ -493,11 +514,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
     if (top > L.lo) {
         uint32_t lo_r, len_r;
         emit_range(L, lo_r, len_r);
-        Event* __restrict__ arena = ev + ev_base(L, c);
+        const uint32_t ab = (uint32_t)ev_base(L, c);
         const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
         const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
         const uint32_t start2 = d_start | (k_start << 16);
-        uint32_t nd = 0, nk = 0, pm = 0xffffffffu;     // "previous byte started an utterance": start rows
+        // "previous byte started an utterance": start rows; a lane cut at hi continues from its halo state
+        uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
+        if (L.chi) {
+            const uint32_t hs = lane_st[2 * c];
+            nd = hs & 0xffffu;
+            nk = hs >> 16;
+            pm = 0;
+        }
         // aligned 64-byte blocks of the ADDRESS space, numbered from the one holding the batch base:
         // block bb covers relative positions [64 bb - r0, 64 bb - r0 + 64)
         const uint32_t r0 = g.r0;
@@ -528,9 +556,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
             SCAN_SUB(w2, 32)
             SCAN_SUB(w1, 16)
             SCAN_SUB(w0, 0)
-            // a lane cut at hi: the state its halo produced for the byte before hi (k_scan_fix checks it
-            // against the state the right neighbour ends with)
-            if (L.chi && bpos == L.hi) lane_st[2 * c] = scan_state(nd, nk);
             if (bb == bb_lo) break;
         }
         if (L.clo) lane_st[2 * c + 1] = scan_state(nd, nk);        // lo is block aligned: state after byte lo
@@ -552,7 +577,7 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
     const Lane L = g_lane(g, c);
     uint32_t lo_r, len_r;
     emit_range(L, lo_r, len_r);
-    Event* __restrict__ arena = ev + ev_base(L, c);
+    const uint32_t ab = (uint32_t)ev_base(L, c);
     const uint32_t nd_words = (uint32_t)(R.SD * R.CDs / 2);
     const uint32_t tk_base = SCAN_TD_BASE + nd_words * 4;
     const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
@@ -574,10 +599,11 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
         nk = lds_u16(ak);
         const bool st = v >= vmin && g_off(g, (uint32_t)v) == b;
         pm = st ? 0xffffffffu : 0u;
-        if ((nd | nk) & 1u) scan_emit(arena, cnt, (uint32_t)b + 1u, lo_r, len_r, ad, ak, tk_base);
+        if ((nd | nk) & 1u) scan_emit(ev, ab, cnt, (uint32_t)b + 1u, lo_r, len_r, ad, ak, tk_base);
         if (st) {
             if ((nd | nk) & 2u)
-                scan_emit(arena, cnt, (uint32_t)b, lo_r, len_r, (nd & 0xfffcu) + eot_d, (nk & 0xfffcu) + eot_k, tk_base);
+                scan_emit(ev, ab, cnt, (uint32_t)b, lo_r, len_r, (nd & 0xfffcu) + eot_d, (nk & 0xfffcu) + eot_k,
+                          tk_base);
             --v;
             while (v >= vmin && g_off(g, (uint32_t)v + 1) == g_off(g, (uint32_t)v)) --v;     // empty rows
         }
@@ -3338,7 +3364,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
             k_lane_count<<<nsb, 256, 0, st>>>(g, e->lane_bkt);
             k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
-            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
+            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, g, text, e->lane_pos, e->bnd, e->lane_st);
             HIPCHK(hipEventRecord(e->kev[0], st));
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
                 R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st);
@@ -3385,8 +3411,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                  uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out,
                  uint64_t out_cap, uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info,
                  hipStream_t st) {
-    if (total_bytes > PII_MAX_BATCH_BYTES) {
-        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
+    if (total_bytes > PII_MAX_BATCH_BYTES || total_bytes + 2ull * n_utt + (total_bytes >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
         return PII_E_ARG;
     }
     e->lane_shift = pick_lane_shift(e, total_bytes);
@@ -3490,8 +3516,8 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         e->err = "window re-scan not enabled (pii_window_enable)";
         return PII_E_ARG;
     }
-    if (total_bytes > PII_MAX_BATCH_BYTES) {
-        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions are 32-bit); split it";
+    if (total_bytes > PII_MAX_BATCH_BYTES || total_bytes + 2ull * n_utt + (total_bytes >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
         return PII_E_ARG;
     }
     e->lane_shift = pick_lane_shift(e, total_bytes);
