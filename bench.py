@@ -320,12 +320,18 @@ def main():
     ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window"], default="scan",
-                    help="scan = config 2 (headline); window = config 3 multi-turn re-scan")
+    ap.add_argument("--workload", choices=["scan", "window", "stream"], default="scan",
+                    help="scan = config 2 (headline); window = config 3 multi-turn re-scan; "
+                         "stream = config 4 PCIe-inclusive batch stream")
     ap.add_argument("--window-n", type=int, default=5)
+    ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
+    ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
+    ap.add_argument("--shard-gb", type=float, default=1.0, help="(config 4) host shard each rank replays, GB")
     args = ap.parse_args()
     if args.workload == "window":
         return window_main(args)
+    if args.workload == "stream":
+        return stream_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
 
@@ -349,6 +355,165 @@ def main():
     def make_engine(batch, bank, C):
         return eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
     line = run_rank(args, rank, world, dev, make_engine, cpu=cpu, dist=dist if world > 1 else None)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- config 4: batch stream
+STREAM_BATCH = 256 << 20      # per-GPU double-buffered batches of 256 MB
+
+
+def _host_ring(args, rank, bank, dev):
+    """One rank's 1 GB host shard (SURVEY config 4: generated in 1 GB shards): conversations
+    [rank*C, (rank+1)*C) in stream order (every conversation's k-th utterance, then the (k+1)-th: a
+    conversation's rows spread over all batches), assembled on the GPU from the utterance bank and
+    copied into pinned host memory, cut into 256 MB batches (HostBatch views of the pinned shard)."""
+    import torch
+    S = importlib.import_module("context-based-pii_amd.stream")
+    U = 100
+    C = max(1, int(args.shard_gb * 1e9 / (U * CFG2_MEAN_LEN)))
+    steps = max(1, int(STREAM_BATCH / (C * CFG2_MEAN_LEN * 1.02)))      # steps of every conversation per batch
+    perm, ranges = synth.stream_order(C, U, steps)
+    meta = synth.reorder(synth.corpus_meta(C, U, bank, seed=synth.SEED + 11, conv_base=rank * C), bank, perm)
+    text, _ = gpu_corpus(meta, bank, dev)
+    n_bytes = int(meta.offsets[-1])
+    h_text = torch.empty(n_bytes + 64, dtype=torch.uint8, pin_memory=True)
+    h_text.copy_(text[:n_bytes + 64])              # device -> pinned host
+    del text
+    offs = meta.offsets.astype(np.int64)
+    slot = (meta.conv_slot - np.uint32(rank * C)).astype(np.int32)
+    batches = []
+    for lo, hi in ranges:
+        b0, b1 = int(offs[lo]), int(offs[hi])
+        pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory()  # noqa: E731
+        batches.append(S.HostBatch(h_text[b0:b1], pin(offs[lo:hi + 1] - b0), pin(slot[lo:hi]), pin(meta.role[lo:hi]),
+                                   pin(meta.ts_us[lo:hi]), hi - lo, b1 - b0))
+    return batches, C, n_bytes
+
+
+def _copy_rate(nbytes, dev, h2d: bool):
+    import torch
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        (d.copy_(h, non_blocking=True) if h2d else h.copy_(d, non_blocking=True))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        (d.copy_(h, non_blocking=True) if h2d else h.copy_(d, non_blocking=True))
+    torch.cuda.synchronize(dev)
+    return 5 * nbytes / (time.perf_counter() - t0) / 1e9
+
+
+def stream_rank(args, rank, world, dev, eng, dist=None, cpu=None):
+    """BASELINE config 4 on one rank: a --stream-gb stream (whole node) sharded by conversation, each
+    rank streaming its share as 256 MB batches from pinned host memory through StreamIngest (H2D of
+    batch i+1 and D2H of batch i-1 overlapped with the scan of batch i).  value = input bytes of all
+    ranks / max-over-ranks wall time, PCIe-inclusive (host buffers in, host buffers out)."""
+    import torch
+    S = importlib.import_module("context-based-pii_amd.stream")
+    bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
+    ring, C, ring_bytes = _host_ring(args, rank, bank, dev)
+    per_rank = args.stream_gb * 1e9 / world
+    K = max(1, int(round(per_rank / (ring_bytes / len(ring)))))
+    ing = S.StreamIngest(eng, max_bytes=max(b.n_bytes for b in ring), max_rows=max(b.n for b in ring))
+    h2d = _copy_rate(STREAM_BATCH, dev, True)
+    d2h = _copy_rate(STREAM_BATCH, dev, False)
+    duplex = h2d + d2h                  # PCIe is full duplex: the two one-way copy rates, summed
+    T = len(eng.type_names)
+    gpu_ms = []
+
+    def consume(i, res):
+        gpu_ms.append(eng.timings()[5])
+    ing.run((ring[i % len(ring)] for i in range(args.warmup)), None)
+    eng.histogram_reset()
+    ing.stats.update(batches=0, bytes_in=0, bytes_out=0, spans=0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    st = ing.run((ring[i % len(ring)] for i in range(K)), consume)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    local = np.zeros(T + 1, dtype=np.int64)
+    local[:T] = eng.histogram().astype(np.int64)
+    local[T] = st["spans"]
+    reduced, verified = local.copy(), bool(local[T] == local[:T].sum())
+    tot_in = st["bytes_in"]
+    if world > 1:
+        t = torch.tensor([elapsed, float(tot_in)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, tot_in = float(t[0].item()), int(t[1].item())
+        h = torch.from_numpy(local).to(dev)
+        dist.all_reduce(h)
+        reduced = h.cpu().numpy()
+        verified = bool(reduced[T] == reduced[:T].sum())
+    names = list(eng.type_names)
+    if rank != 0:
+        return None
+    mean_b = st["bytes_in"] / max(st["batches"], 1)
+    gpu_s = float(np.mean(gpu_ms)) / 1e3 if gpu_ms else 0.0
+    serial = mean_b / (h2d * 1e9) + gpu_s + (st["bytes_out"] / max(st["batches"], 1)) / (d2h * 1e9)
+    per_batch = elapsed / max(st["batches"], 1)
+    rows_total = sum(ring[i % len(ring)].n for i in range(K))
+    # over PCIe per row: in offsets 8 + slot 4 + role 1 + ts 8; out offsets 8 + ctx 2; + 16 B per span
+    pcie_GBps = (st["bytes_in"] + st["bytes_out"] + 31 * rows_total + 16 * st["spans"]) / elapsed / 1e9
+    return {
+        "metric": "config 4 stream: transcript MB/s scanned+redacted per node, PCIe-inclusive (host in, host out)",
+        "value": round(tot_in / elapsed / 1e6, 1), "unit": "MB/s", "n_gpus": world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(per_batch * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak" if args.stream_weak else "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"config4: {args.stream_gb:g} GB stream per node sharded by conversation, 256 MB "
+                               f"double-buffered batches from pinned host memory (each rank replays its 1 GB shard, "
+                               f"{C} conversations x 100 utterances in stream order)",
+                   "batch_bytes": int(mean_b), "batches_per_gpu": K, "bytes_per_gpu": int(st["bytes_in"]),
+                   "parallelism": f"conversation-sharded x{world}"},
+        "overlap": {"h2d_GBps_alone": round(h2d, 2), "d2h_GBps_alone": round(d2h, 2),
+                    "gpu_ms_per_batch": round(gpu_s * 1e3, 3), "wall_ms_per_batch": round(per_batch * 1e3, 3),
+                    "serial_ms_per_batch": round(serial * 1e3, 3),
+                    "overlap_factor": round(serial / max(per_batch, 1e-12), 3),
+                    "bound": "pcie h2d" if mean_b / (h2d * 1e9) >= gpu_s else "gpu"},
+        "roofline": {"bound": "pcie", "achieved": round(pcie_GBps, 2), "peak": round(duplex, 2),
+                     "unit": "GB/s", "frac": round(pcie_GBps / duplex, 4), "traffic": None,
+                     "note": "(input + output + per-row arrays) bytes over PCIe / wall, vs the sum of the measured "
+                             "one-way pinned copy rates of a 256 MB batch (H2D + D2H, full duplex)"},
+        "capacity_reruns": st["capacity_reruns"],
+        "histogram": {"collective": "all_reduce u64[T+1] (RCCL)" if world > 1 else "none (1 rank)",
+                      "total_spans": int(reduced[T]), "verified": verified,
+                      "per_type": {names[t]: int(reduced[t]) for t in range(T) if reduced[t]}},
+        "cpu_baseline": cpu,
+    }
+
+
+def stream_main(args):
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stream_weak:
+        args.stream_gb = args.stream_gb * world
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
+        cpu = cpu_baseline(bank, args.cpu_gb * 1e9)
+    import torch
+    import torch.distributed as dist
+    eng_mod = importlib.import_module("context-based-pii_amd.engine")
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comp = compiler.compile_default()
+    C = max(1, int(args.shard_gb * 1e9 / (100 * CFG2_MEAN_LEN)))
+    eng = eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
+    line = stream_rank(args, rank, world, dev, eng, dist=dist if world > 1 else None, cpu=cpu)
+    eng.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -49,7 +49,11 @@ constexpr uint32_t MIN_LANE_SHIFT = 7;        // smallest scan lane, 128 B (smal
 constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
-enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16, ERR_STITCH = 32 };
+enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16, ERR_STITCH = 32,
+                  ERR_ARGS = 64 };
+// a call whose declared batch size was wrong (ERR_ARGS) or whose queues overflowed (ERR_QUEUE, re-run by
+// pii_sync) stops every later stage
+constexpr uint32_t ERR_ABORT = ERR_QUEUE | ERR_ARGS;
 
 struct Event {
     uint32_t pos;   // candidate start, relative to the batch base
@@ -157,10 +161,14 @@ __global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* 
                               uint32_t n_chunks, uint32_t lane_shift, uint32_t r0, uint32_t long_min, int kw_always,
                               uint32_t* __restrict__ first_utt, uint32_t* __restrict__ out_len,
                               int32_t* __restrict__ kw, uint32_t* __restrict__ wc_n,
-                              uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count) {
+                              uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count,
+                              uint64_t decl_base, uint64_t decl_bytes, uint32_t* __restrict__ err) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u > n_utt) return;
     const uint64_t base = offs[0];
+    // the caller declared offsets[0] and the batch size (no host round trip): every later kernel sized
+    // its work from them, so a wrong declaration stops the call
+    if (u == n_utt && (base != decl_base || offs[n_utt] - base != decl_bytes)) atomicOr(err, (uint32_t)ERR_ARGS);
     const uint64_t su = offs[u] - base + r0;
     uint64_t c_lo = 0;
     if (u > 0) c_lo = ((offs[u - 1] - base + r0) >> lane_shift) + 1;
@@ -486,8 +494,10 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
-                                                     uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st) {
+                                                     uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
+                                                     const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+    if (*err & ERR_ARGS) return;              // the declared batch size was wrong: nothing is sized for it
     uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
     const int nd_words = R.SD * R.CDs / 2;      // rows padded to an even class count
     const int nk_words = R.SK * R.CKs / 2;
@@ -631,7 +641,7 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g,
     uint32_t& s_np = s_prev[FIX_Q + 1];
     uint32_t& s_full = s_prev[FIX_Q + 2];
     const uint32_t nrows = *long_count;
-    if (blockIdx.x >= nrows) return;
+    if (blockIdx.x >= nrows || (*err & ERR_ARGS)) return;
     {
         const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
@@ -918,6 +928,7 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
     __shared__ uint32_t s_acc_off[256];
     __shared__ uint16_t s_kmin[256];
+    if (*err & ERR_ARGS) return;
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t n_chunks = g.n_chunks;
@@ -1041,7 +1052,7 @@ __global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs*
                                                 const uint64_t* __restrict__ ev_count, const uint32_t* __restrict__ err,
                                                 PairRes* __restrict__ pres) {
     __shared__ uint32_t s_off[257];
-    if (*err & ERR_QUEUE) return;           // a queue overflowed: records are incomplete, the batch re-runs
+    if (*err & ERR_ABORT) return;           // a queue overflowed: records are incomplete, the batch re-runs
     __shared__ uint16_t s_ids[2048];
     const uint32_t n_dacc = R.n_dacc;
     const bool small = n_dacc < 256 && R.d_acc_off[n_dacc] <= 2048;
@@ -1114,7 +1125,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restri
                                                            const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     __shared__ uint32_t s_mc[PAIR_WAVES], s_cc[PAIR_WAVES + 1];
-    if (*err & ERR_QUEUE) {
+    if (*err & ERR_ABORT) {
         if (threadIdx.x < PAIR_WAVES) mcount[blockIdx.x * PAIR_WAVES + threadIdx.x] = 0;
         return;
     }
@@ -1545,7 +1556,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 const Geo g, const SelIO io, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & ERR_QUEUE) return;           // the batch is re-run with a larger queue
+    if (*err & ERR_ABORT) return;           // the batch is re-run with a larger queue
     const uint8_t* lb = load_image(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1579,7 +1590,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint
                                                         uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     __shared__ uint32_t sh[ROW_BLOCK / 64];
     __shared__ uint32_t s_carry;
-    if (*err & ERR_QUEUE) return;
+    if (*err & ERR_ABORT) return;
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         uint32_t ca, kb;
         int64_t s_r, e_r;
@@ -1611,7 +1622,7 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
                                                  const uint32_t* __restrict__ long_count,
                                                  const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & ERR_QUEUE) return;
+    if (*err & ERR_ABORT) return;
     const uint8_t* lb = load_image(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
@@ -1635,7 +1646,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_rowlen(const Geo g, const uint32_
                                                      uint32_t* __restrict__ out_len, const uint32_t* __restrict__ err) {
     __shared__ int32_t sh[ROW_BLOCK / 64];
     __shared__ int32_t s_carry;
-    if (*err & ERR_QUEUE) return;
+    if (*err & ERR_ABORT) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         const uint32_t r = long_rows[ri];
@@ -2385,7 +2396,7 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
                                                    uint64_t pair_cap, int n_pat, WCand* __restrict__ wc,
                                                    uint32_t* __restrict__ wc_first, uint32_t* __restrict__ wc_n,
                                                    const uint32_t* __restrict__ err) {
-    if (*err & ERR_QUEUE) return;
+    if (*err & ERR_ABORT) return;
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     const uint32_t np = lane_np[c];
@@ -2504,7 +2515,7 @@ __global__ __launch_bounds__(256) void k_win_halo(const uint4* __restrict__ img,
                                                   const WinBatch B, WCand* __restrict__ wc,
                                                   const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & (ERR_QUEUE | ERR_SLOT)) return;
+    if (*err & (ERR_ABORT | ERR_SLOT)) return;
     const uint8_t* lb = load_image(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
@@ -2558,7 +2569,7 @@ __global__ __launch_bounds__(256) void k_win_plan(const WinRing W, const WinBatc
     z.off = 0xffffffffu;
     z.ri = z.cnt = z.head = 0;
     wnew[u] = z;
-    if (*err & (ERR_QUEUE | ERR_SLOT)) {
+    if (*err & (ERR_ABORT | ERR_SLOT)) {
         bound[u] = 0;
         return;
     }
@@ -2578,7 +2589,7 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
                                                     pii_span* __restrict__ wfd, uint32_t* __restrict__ n_wfind,
                                                     uint32_t* __restrict__ wout_len, uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & (ERR_QUEUE | ERR_SLOT)) return;
+    if (*err & (ERR_ABORT | ERR_SLOT)) return;
     const uint8_t* lb = load_image(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[WS_TRANS]), lb + li.off[WS_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[WS_HDESC]);
@@ -2718,7 +2729,7 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
 __global__ __launch_bounds__(256) void k_win_alloc(const WinRing W, const WinBatch B, WNew* __restrict__ wnew,
                                                    uint32_t* __restrict__ err) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= B.n_utt || (*err & (ERR_QUEUE | ERR_SLOT))) return;
+    if (u >= B.n_utt || (*err & (ERR_ABORT | ERR_SLOT))) return;
     const uint32_t sl = B.slot[u];
     if (sl >= W.n_slots || (u + 1 < B.n_utt && B.slot[u + 1] == sl)) return;
     uint32_t k = 1;
@@ -3358,7 +3369,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
                                                                 e->long_min, R.kw_always_min, e->first_utt,
                                                                 e->out_len, e->kw, win_ctx ? e->wc_n : nullptr,
-                                                                e->long_rows, e->long_count);
+                                                                e->long_rows, e->long_count, base, total_bytes, e->d_err);
         if (n_chunks > 0) {
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
@@ -3367,7 +3378,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, g, text, e->lane_pos, e->bnd, e->lane_st);
             HIPCHK(hipEventRecord(e->kev[0], st));
             k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
-                R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st);
+                R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st, e->d_err);
             HIPCHK(hipEventRecord(e->kev[1], st));
             if (e->long_min != NO_CUTS)
                 k_scan_fix<<<row_grid(e, total_bytes), 256, e->scan_lds + FIX_LDS, st>>>(
@@ -3594,7 +3605,8 @@ int rerun_last(pii_engine* e) {
 
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
                 const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
-                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream);
+                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream,
+                const uint64_t* declared);
 }  // namespace
 
 extern "C" {
@@ -3968,13 +3980,44 @@ int pii_scan_redact_device(pii_engine* e, const uint8_t* d_bytes, const uint64_t
                            uint64_t out_cap, uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
                            int16_t* d_ctx_info, void* stream) {
     return device_call(e, false, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,
-                       d_spans, span_cap, d_ctx_info, stream);
+                       d_spans, span_cap, d_ctx_info, stream, nullptr);
+}
+
+int pii_scan_redact_device_ex(pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                              uint64_t batch_base, uint64_t batch_bytes, const uint32_t* d_slot, const uint8_t* d_role,
+                              const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_offsets,
+                              pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream) {
+    const uint64_t decl[2] = {batch_base, batch_bytes};
+    return device_call(e, false, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,
+                       d_spans, span_cap, d_ctx_info, stream, decl);
+}
+
+int pii_reserve(pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint64_t max_out, uint32_t max_spans) {
+    if (!e) return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    // the most lanes any batch of at most max_bytes can have: big batches take 1 KiB lanes, smaller
+    // ones shrink the lanes to keep at least n_cu*256 of them (pick_lane_shift), i.e. < 2*n_cu*256
+    const uint32_t sh = pick_lane_shift(e, max_bytes);
+    uint64_t lanes = std::max<uint64_t>(((max_bytes + 63) >> sh) + 2, 2ull * e->n_cu * 256 + 2);
+    lanes = std::min<uint64_t>(lanes, ((max_bytes + 63) >> MIN_LANE_SHIFT) + 2);
+    int rc;
+    if ((rc = ensure_scratch(e, max_utt, max_bytes, (uint32_t)std::min<uint64_t>(lanes, 0xffffffffull))) ||
+        (rc = ensure_queues(e, max_bytes)) || (rc = ensure_redact(e, max_spans, max_out)))
+        return rc;
+    if (e->lb_cap < LB_MAX_TILES + 64) {      // the look-back scan's tile states (exclusive_scan)
+        if ((rc = grow(e, e->lb_state, (size_t)LB_MAX_TILES + 64))) return rc;
+        HIPCHK(hipMemsetAsync(e->lb_state, 0, ((size_t)LB_MAX_TILES + 64) * 8, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->lb_cap = LB_MAX_TILES + 64;
+    }
+    return PII_OK;
 }
 
 int pii_sync(pii_engine* e, uint64_t totals[3]) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipEventSynchronize(e->tev[6]));
-    for (int attempt = 0; (e->h_totals[2] & ERR_QUEUE) && attempt < 4; ++attempt) {
+    for (int attempt = 0; (e->h_totals[2] & ERR_QUEUE) && !(e->h_totals[2] & ERR_ARGS) && attempt < 4; ++attempt) {
         // a work queue overflowed (pair queue, event records, window findings): grow it to the exact
         // need and run the batch again (context and window history were not committed, so the re-run
         // is idempotent)
@@ -4014,6 +4057,10 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         totals[2] = e->h_totals[2];
     }
     const uint64_t f = e->h_totals[2];
+    if (f & ERR_ARGS) {
+        e->err = "declared batch base / size do not match offsets[0] / offsets[n_utt] - offsets[0]";
+        return PII_E_ARG;
+    }
     if (f & ERR_SLOT) return PII_E_ARG;
     if (f & ERR_RING) {
         e->err = "a conversation's re-scan window does not fit its history slot; raise slot_bytes (pii_window_enable)";
@@ -4129,15 +4176,21 @@ int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* 
 
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
                 const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
-                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream) {
+                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream,
+                const uint64_t* declared = nullptr) {
     if (!e || !d_offsets || !d_slot || !d_role || !d_out_offsets) return PII_E_ARG;
     if (n_utt > 0 && (!d_bytes || !d_out || !d_spans)) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
     uint64_t tb[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(tb, d_offsets, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(tb + 1, d_offsets + n_utt, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (declared) {          // the caller states offsets[0] and the batch size: no host round trip
+        tb[0] = declared[0];
+        tb[1] = declared[0] + declared[1];
+    } else {
+        HIPCHK(hipMemcpyAsync(tb, d_offsets, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(tb + 1, d_offsets + n_utt, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     if (tb[1] < tb[0]) return PII_E_ARG;
     return (window ? run_window : run_pipeline)(e, d_bytes, d_offsets, n_utt, tb[0], tb[1] - tb[0], d_slot, d_role,
                                                 d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx_info, st);
@@ -4208,7 +4261,7 @@ int pii_rescan_window_device(pii_engine* e, const uint8_t* d_bytes, const uint64
                              uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets, pii_span* d_spans,
                              uint32_t span_cap, int16_t* d_win_ctx, void* stream) {
     return device_call(e, true, d_bytes, d_offsets, n_utt, d_conv_slot, d_role, d_ts_us, d_out_bytes, out_cap,
-                       d_out_offsets, d_spans, span_cap, d_win_ctx, stream);
+                       d_out_offsets, d_spans, span_cap, d_win_ctx, stream, nullptr);
 }
 
 int pii_context_get(pii_engine* e, uint32_t slot, int32_t* group, int64_t* ts_us) {

@@ -21,7 +21,8 @@ ROLE_CUSTOMER, ROLE_AGENT, ROLE_OTHER = 0, 1, 2
 ERROR_NAMES = {PII_E_ARG: "PII_E_ARG", PII_E_RULES: "PII_E_RULES", PII_E_DEVICE: "PII_E_DEVICE",
                PII_E_CAPACITY: "PII_E_CAPACITY", PII_E_ORDER: "PII_E_ORDER", PII_E_NOMEM: "PII_E_NOMEM"}
 EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_type_name", "pii_context_group_type",
-           "pii_last_error", "pii_scan_redact", "pii_scan_redact_device", "pii_sync", "pii_context_get",
+           "pii_last_error", "pii_scan_redact", "pii_scan_redact_device", "pii_scan_redact_device_ex",
+           "pii_reserve", "pii_sync", "pii_context_get",
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device"]
@@ -79,6 +80,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_scan_redact.argtypes = [P, P, P, c.c_uint32, P, P, P, P, c.c_uint64, P, P, c.c_uint32,
                                     c.POINTER(c.c_uint32), P]
     lib.pii_scan_redact_device.argtypes = [P, P, P, c.c_uint32, P, P, P, P, c.c_uint64, P, P, c.c_uint32, P, P]
+    lib.pii_scan_redact_device_ex.argtypes = [P, P, P, c.c_uint32, c.c_uint64, c.c_uint64, P, P, P, P, c.c_uint64,
+                                              P, P, c.c_uint32, P, P]
+    lib.pii_reserve.argtypes = [P, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32]
     lib.pii_sync.argtypes = [P, U64]
     lib.pii_context_get.argtypes = [P, c.c_uint32, I32, I64]
     lib.pii_context_set.argtypes = [P, c.c_uint32, c.c_int32, c.c_int64]
@@ -242,6 +246,22 @@ class Engine:
                                              out_cap, d_out_offsets, d_spans, span_cap, d_ctx, stream)
         if rc != PII_OK:
             raise self._err(rc, "pii_scan_redact_device")
+
+    def scan_redact_device_ex(self, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot, d_role, d_ts, d_out,
+                              out_cap, d_out_offsets, d_spans, span_cap, d_ctx=None, stream=None) -> None:
+        """scan_redact_device with offsets[0] and the batch size stated by the caller: enqueues without
+        any device-to-host read (pii_scan_redact_device_ex)."""
+        rc = self.lib.pii_scan_redact_device_ex(self.h, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot,
+                                                d_role, d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx,
+                                                stream)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_scan_redact_device_ex")
+
+    def reserve(self, max_utt: int, max_bytes: int, max_out: int, max_spans: int) -> None:
+        """pre-size the work buffers so calls within these bounds allocate nothing (pii_reserve)"""
+        rc = self.lib.pii_reserve(self.h, max_utt, max_bytes, max_out, max_spans)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_reserve")
 
     def sync(self) -> Tuple[int, int, int]:
         tot = (ctypes.c_uint64 * 3)()

@@ -306,6 +306,30 @@ def make_corpus(n_conv: int, utt_per_conv: int, bank: Bank, seed: int = SEED, co
     return Corpus(gather_bytes(m, bank), m.offsets, m.conv_slot, m.role, m.ts_us, m.bank_id)
 
 
+def reorder(meta: CorpusMeta, bank: Bank, perm: np.ndarray) -> CorpusMeta:
+    """rows of `meta` in the order `perm` (offsets recomputed)"""
+    bid = meta.bank_id[perm]
+    lens = (bank.offsets[1:] - bank.offsets[:-1])[bid]
+    offs = np.zeros(len(bid) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return CorpusMeta(bid, offs, meta.conv_slot[perm], meta.role[perm], meta.ts_us[perm])
+
+
+def stream_order(n_conv: int, utt_per_conv: int, steps_per_batch: int) -> Tuple[np.ndarray, List[Tuple[int, int]]]:
+    """Config 4 stream order of a conversation-major corpus: batch b carries steps
+    [b*s, (b+1)*s) of every conversation (a conversation's rows spread over all batches), and inside
+    a batch a conversation's rows are contiguous (the engine's batch contract).  Returns the row
+    permutation and the [lo, hi) row range of every batch."""
+    perm, ranges, lo = [], [], 0
+    for k0 in range(0, utt_per_conv, steps_per_batch):
+        k1 = min(utt_per_conv, k0 + steps_per_batch)
+        p = (np.arange(n_conv, dtype=np.int64)[:, None] * utt_per_conv + np.arange(k0, k1)[None, :]).reshape(-1)
+        perm.append(p)
+        ranges.append((lo, lo + len(p)))
+        lo += len(p)
+    return np.concatenate(perm), ranges
+
+
 def step_major(meta: CorpusMeta, bank: Bank, n_conv: int, utt_per_conv: int) -> CorpusMeta:
     """The same rows streamed the way the aggregator sees them (config 3): step k = the k-th
     utterance of every conversation, so rows [k*n_conv, (k+1)*n_conv) are one re-scan call."""

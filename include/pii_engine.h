@@ -108,6 +108,22 @@ int pii_scan_redact_device(struct pii_engine* e, const uint8_t* d_bytes, const u
                            const int64_t* d_ts_us, uint8_t* d_out_bytes, uint64_t out_cap,
                            uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
                            int16_t* d_ctx_info, void* stream);
+/* The same call with the batch's offsets[0] (batch_base) and byte size (offsets[n_utt] - offsets[0])
+ * stated by the caller, so that enqueueing it needs no device-to-host read (pii_scan_redact_device
+ * reads the two offsets back and waits for them).  A streaming ingest (config 4: the reference's
+ * Pub/Sub -> subscriber -> handler chain, main_service/main.py:522-562 -> :386-425 -> :580, one DLP
+ * RPC per message) enqueues batch i+1 while batch i's output is still being copied out.  A wrong
+ * declaration is detected on the device and pii_sync() returns PII_E_ARG; nothing is committed. */
+int pii_scan_redact_device_ex(struct pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                              uint32_t n_utt, uint64_t batch_base, uint64_t batch_bytes,
+                              const uint32_t* d_conv_slot, const uint8_t* d_role, const int64_t* d_ts_us,
+                              uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets,
+                              pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream);
+/* Pre-size every internal work buffer for batches of at most max_utt rows / max_bytes input bytes /
+ * max_out output bytes / max_spans spans, so that calls within those bounds allocate nothing (no
+ * hipMalloc, which synchronizes the device, inside a streaming loop).  The pair / event queues still
+ * grow on overflow (pii_sync re-runs the batch) -- their need depends on the text, not its size. */
+int pii_reserve(struct pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint64_t max_out, uint32_t max_spans);
 /* wait for the last device call; totals[0] = output bytes, [1] = spans, [2] = error flags */
 int pii_sync(struct pii_engine* e, uint64_t totals[3]);
 
