@@ -43,7 +43,7 @@ def _cpu_init(data, offs, role, conv, ts):
 
 def _cpu_work(rng):
     from oracle import pii_oracle as O
-    cfg = O.RuleConfig.load()
+    cfg = O.RuleConfig.load(_CPU.get("cfg_path"))
     d, o, r, c, t = _CPU["data"], _CPU["offs"], _CPU["role"], _CPU["conv"], _CPU["ts"]
     lo, hi = rng
     rows = [(int(c[i]), int(r[i]), d[int(o[i]):int(o[i + 1])].tobytes(), int(t[i])) for i in range(lo, hi)]
@@ -80,7 +80,7 @@ def host_cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(bank, min_bytes: float = 1e9):
+def cpu_baseline(bank, min_bytes: float = 1e9, cfg_path=None, what="config-2"):
     """The oracle (Python re + validators), multi-process over whole conversations on this host's CPU
     share, timed over at least `min_bytes` of the same synthetic distribution (SURVEY §8(d) /
     BASELINE.md §2: the full 1.2 GB config would take minutes, so >= 1 GB is timed and reported as a
@@ -92,6 +92,7 @@ def cpu_baseline(bank, min_bytes: float = 1e9):
     offs = meta.offsets.astype(np.int64)
     blocks = [(c * 100, min(c + 50, n_conv) * 100) for c in range(0, n_conv, 50)]   # 50 conversations each
     ctx = mp.get_context("fork")
+    _CPU["cfg_path"] = cfg_path
     t0 = time.perf_counter()
     with ctx.Pool(cores, initializer=_cpu_init, initargs=(data, offs, meta.role, meta.conv_slot, meta.ts_us)) as pool:
         res = pool.map(_cpu_work, blocks, chunksize=1)
@@ -99,7 +100,7 @@ def cpu_baseline(bank, min_bytes: float = 1e9):
     nbytes = sum(b for _, b in res)
     return {"value": round(nbytes / wall / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
             "host_cpu": host_cpu_model(), "host_logical_cpus": os.cpu_count(),
-            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e9:.3f} GB) of the config-2 synthetic "
+            "sample": f"{n_conv} conversations x 100 utterances ({nbytes / 1e9:.3f} GB) of the {what} synthetic "
                       f"distribution, oracle/pii_oracle.py process_rows over whole conversations, multiprocessing "
                       f"fork pool of {cores} (this host's CPU share), wall {wall:.1f}s; the 1.208 GB config-2 batch "
                       f"extrapolates to {1.208e9 / (nbytes / wall):.1f}s"}
@@ -161,7 +162,7 @@ class DeviceBatch:
     corpus (gpu = conversation_id % G on a dense id space is a contiguous block here),
     staged into device memory once, plus the output buffers."""
 
-    def __init__(self, C, U, bank, conv_base, dev):
+    def __init__(self, C, U, bank, conv_base, dev, join: int = 1):
         import torch
         self.meta = synth.corpus_meta(C, U, bank, seed=synth.SEED, conv_base=conv_base)
         self.text, self.offs = gpu_corpus(self.meta, bank, dev)
@@ -170,6 +171,15 @@ class DeviceBatch:
         self.slot = torch.from_numpy((self.meta.conv_slot - conv_base).view(np.int32)).to(dev)
         self.role = torch.from_numpy(self.meta.role).to(dev)
         self.ts = torch.from_numpy(self.meta.ts_us).to(dev)
+        if join > 1:
+            # long rows (whole transcripts, ccai_insights_function/main.py:47-50): every `join`
+            # consecutive utterances form one row, redacted without role context (ROLE_OTHER)
+            idx = np.unique(np.append(np.arange(0, self.n + 1, join), self.n))
+            self.offs = self.offs[torch.from_numpy(idx).to(dev)].contiguous()
+            self.n = len(idx) - 1
+            self.slot = torch.arange(self.n, dtype=torch.int32, device=dev) % max(C, 1)
+            self.role = torch.full((self.n,), 2, dtype=torch.uint8, device=dev)
+            self.ts = self.ts[:self.n].contiguous()
         self.out_cap = self.n_bytes + 48 * self.n
         self.span_cap = self.n * 2
         self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
@@ -183,16 +193,18 @@ class DeviceBatch:
                                self.out_offs.data_ptr(), self.spans.data_ptr(), self.span_cap, self.ctx.data_ptr())
 
 
-def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None):
+def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None, bank=None):
     """One rank of the config-2 benchmark: shard -> W warmup steps -> K timed steps between barriers
     + device syncs -> max-over-ranks time.  A step = one scan+redact pass over the rank's resident
     shard + the all-reduce of the u64[T+1] per-infoType histogram (the only collective; reset every
     step).  After timing, the reduced histogram of the last step is checked against an all-gather
     of every rank's own counts.  Returns the JSON line on rank 0 (None elsewhere)."""
     import torch
-    bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
+    if bank is None:
+        bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
     C, U = args.conversations, args.utt_per_conv
-    B = DeviceBatch(C, U, bank, rank * C, dev)
+    join = max(1, int(getattr(args, "row_kb", 0) * 1024 / CFG2_MEAN_LEN)) if getattr(args, "workload", "") == "long" else 1
+    B = DeviceBatch(C, U, bank, rank * C, dev, join=join)
     eng = make_engine(B, bank, C)
     T = len(eng.type_names)
     hist = torch.zeros(T + 1, dtype=torch.int64, device=dev)
@@ -268,10 +280,15 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None)
         "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "config2: per GPU 100k conversations x 100 utterances (10M utterances, "
-                               "~120 B lognormal) single-utterance scan+redact with expected_pii_type context",
+        "config": {"workload": getattr(args, "workload_desc", None) or
+                   "config2: per GPU 100k conversations x 100 utterances (10M utterances, "
+                   "~120 B lognormal) single-utterance scan+redact with expected_pii_type context"
+                   if join == 1 else
+                   f"long rows: the config-2 bytes as {n} rows of ~{args.row_kb} KiB (whole transcripts, {join} "
+                   f"utterances each, no role context), cut into halo-scanned lanes",
                    "utterances_per_gpu": n, "bytes_per_gpu": n_bytes, "parallelism": f"conversation-sharded x{world}",
-                   "rules": "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
+                   "rules": getattr(args, "rules_desc", None) or
+                   "main_service/dlp_config.yaml + rules/builtin_infotypes.yaml"},
         "utt_per_s": round(n * world * args.steps / elapsed, 1),
         "spans_per_step_per_gpu": int(ns),
         "queues_per_step_per_gpu": {"scan_events": n_events, "candidate_pairs": n_pairs},
@@ -320,9 +337,11 @@ def main():
     ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window", "stream"], default="scan",
+    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5"], default="scan",
                     help="scan = config 2 (headline); window = config 3 multi-turn re-scan; "
-                         "stream = config 4 PCIe-inclusive batch stream")
+                         "stream = config 4 PCIe-inclusive batch stream; long = config-2 bytes as long rows; "
+                         "config5 = 500+ custom regex / dictionary infoTypes")
+    ap.add_argument("--row-kb", type=int, default=1024, help="(long) row size, KiB")
     ap.add_argument("--window-n", type=int, default=5)
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
     ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
@@ -332,6 +351,8 @@ def main():
         return window_main(args)
     if args.workload == "stream":
         return stream_main(args)
+    if args.workload == "config5":
+        return config5_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
 
@@ -359,6 +380,62 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- config 5: 500+ types
+def config5_main(args):
+    """BASELINE config 5: the config-2 shape (conversations x 100 utterances, one scan+redact pass per
+    step) over a seeded rule set of 520 custom regex / dictionary infoTypes + the shipped ones
+    (rulegen.Config5), text drawn from a bank of config-5 utterances.  The rule set is split over
+    several SCAN groups (one k_scan pass each) and its FIRST automata are read from global memory
+    (L2-resident); the L2 hit rate of those kernels comes from a committed PMC pass (profiles/)."""
+    import tempfile
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
+    rulegen = importlib.import_module("context-based-pii_amd.rulegen")
+    c5 = rulegen.Config5()
+    path = os.path.join(tempfile.gettempdir(), f"config5_{os.getpid()}.json")
+    c5.save(path)
+    bank = c5.build_bank()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(bank, args.cpu_gb * 1e9, cfg_path=path, what="config-5")
+    import torch
+    import torch.distributed as dist
+    eng_mod = importlib.import_module("context-based-pii_amd.engine")
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comp = compiler.compile_rules(compiler.Rules.load(path))
+    args.workload_desc = (f"config5: per GPU {args.conversations} conversations x {args.utt_per_conv} utterances "
+                          f"of config-5 text, scan+redact over {len(comp.rules.type_names)} infoTypes "
+                          f"({len(comp.rules.patterns)} detector patterns in {len(comp.scan_groups)} SCAN groups)")
+    args.rules_desc = "rules/dlp_config.json + rulegen.Config5(n_regex=320, n_dict=200, seed=5)"
+
+    def make_engine(batch, bank_, C):
+        return eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
+    line = run_rank(args, rank, world, dev, make_engine, cpu=cpu, dist=dist if world > 1 else None, bank=bank)
+    if rank == 0:
+        line["metric"] = "config 5: transcript MB/s scanned+redacted per node with 500+ custom infoTypes"
+        line["l2"] = measured_l2()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    os.unlink(path)
+
+
+def measured_l2():
+    """TCC hit rate of the config-5 kernels from the committed PMC pass (tools/pmc_l2.py), if it was
+    measured on these kernel sources"""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "config5_l2.json")))
+    except (OSError, ValueError):
+        return None
+    return t if t.get("source_digest") == source_digest() else None
 
 
 # --------------------------------------------------------------------------- config 4: batch stream

@@ -484,12 +484,16 @@ class MealyDFA:
         return self.trans.shape[1] - 1
 
 
-def build_mealy_dfa(nfa: NFA, starts: Sequence[int], max_states: int = 32767) -> MealyDFA:
+def build_mealy_dfa(nfa: NFA, starts: Sequence[int], max_states: int = 32767,
+                    max_bytes: Optional[int] = None) -> MealyDFA:
     """Unanchored set-semantics DFA with accepts on TRANSITIONS.  Transition (q, c) reports the
     patterns whose match ends right before c in scan direction (for the reverse SCAN: whose match
-    STARTS right after c in text order)."""
+    STARTS right after c in text order).  `max_bytes` bounds the u16 table (rows padded to an even
+    class count) and fails early (RuleError) when the subset construction exceeds it."""
     cmap, reps = byte_classes(nfa)
     ncls = len(reps)
+    if max_bytes is not None:
+        max_states = min(max_states, max_bytes // (2 * ((ncls + 2) & ~1)) * 2)
     ckind = [_kind_of_byte(r) for r in reps]
     start_set = frozenset(starts)
     index: Dict[tuple, int] = {}
@@ -833,6 +837,7 @@ class Compiled:
     hot_rules: List[HotRule]
     sections: "OrderedDict[str, np.ndarray]"
     blob: bytes
+    scan_groups: List[List[int]] = None     # pattern ids of each SCAN group (group 0 first)
 
 
 SCAN_BUDGET = 3     # prefix characters per detector pattern in the SCAN prefilter
@@ -848,21 +853,91 @@ def _acc_tables(m: MealyDFA):
     return off, np.array(ids or [0], dtype=np.uint16)
 
 
+SCAN_LDS_BYTES = 65536          # k_scan tables: u16 LDS byte addresses (class map + D rows + K rows)
+SCAN_CMAP_BYTES = 1024
+SCAN_GROUP_BYTES = 62 * 1024    # D table of a scan group >= 1 (its K is a 1-row never-accepting stub)
+SCAN_GROUPS_MAX = 8             # k_pairs merges at most this many per-group event lists per lane
+
+
+def _table_bytes(m: MealyDFA) -> int:
+    return m.n_states * ((m.n_classes + 2) & ~1) * 2
+
+
+def _scan_dfa(patterns: Sequence[Pattern], budget: int, max_bytes: Optional[int] = None) -> Optional[MealyDFA]:
+    nd = NFA()
+    sd = [add_relaxed(nd, p.pattern, p.pid, budget, reverse=True) for p in patterns]
+    try:
+        m = build_mealy_dfa(nd, sd, max_bytes=max_bytes)
+    except RuleError:
+        if max_bytes is None:
+            raise
+        return None
+    return m if max_bytes is None or _table_bytes(m) <= max_bytes else None
+
+
+def _prefix_key(p: Pattern) -> str:
+    return re.sub(r"^\(\?i\)|\\b", "", p.pattern).lower()
+
+
+def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List[Pattern], MealyDFA]]:
+    """Split the detector patterns over reverse D automata that each fit k_scan's LDS (config 5: 500+
+    custom types).  One automaton per independent pattern set multiplies the states (a product of
+    the sets' tries), so large rule sets get several smaller automata, each stepped by its own
+    k_scan pass.  Group 0 is stepped together with the keyword automaton K and holds every built-in
+    and excluder pattern; the rest, ordered by prefix so that similar prefixes share states, is cut
+    in halves until each half fits."""
+    limit0 = SCAN_LDS_BYTES - SCAN_CMAP_BYTES - k_bytes
+    whole = _scan_dfa(rules.patterns, budget, limit0) if len(rules.patterns) <= 256 else None
+    if whole is not None:
+        return [(list(rules.patterns), whole)]
+    excl = set()
+    for insp in rules.variants():
+        for rs in insp.get("rule_set", []) or []:
+            for rule in rs.get("rules", []):
+                if "exclusion_rule" in rule:
+                    excl |= {it["name"] for it in rule["exclusion_rule"].get("exclude_info_types", {}).get(
+                        "info_types", [])}
+    base = [p for p in rules.patterns if not p.custom or p.type_name in excl]
+    rest = sorted((p for p in rules.patterns if p.custom and p.type_name not in excl), key=_prefix_key)
+    g0 = _scan_dfa(base, budget, limit0)
+    if g0 is None:
+        raise RuleError("the built-in detectors' SCAN automaton does not fit k_scan's LDS")
+    out = [(base, g0)]
+
+    def split(pats):
+        m = _scan_dfa(pats, budget, SCAN_GROUP_BYTES)
+        if m is not None:
+            out.append((pats, m))
+            return
+        if len(pats) == 1:
+            raise RuleError(f"the SCAN automaton of {pats[0].type_name} alone does not fit k_scan's LDS")
+        h = len(pats) // 2
+        split(pats[:h])
+        split(pats[h:])
+    if rest:
+        split(rest)
+    if len(out) > SCAN_GROUPS_MAX:
+        raise RuleError(f"{len(out)} SCAN groups (more than {SCAN_GROUPS_MAX})")
+    return out
+
+
 def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     P = len(rules.patterns)
     G = len(rules.kw_groups)
     if P == 0:
         raise RuleError("no detectors")
     # ---- SCAN (two Mealy automata stepped together, right to left) ----
-    nd = NFA()
-    sd = [add_relaxed(nd, p.pattern, p.pid, scan_budget, reverse=True) for p in rules.patterns]
-    scan_d = build_mealy_dfa(nd, sd)
     nk = NFA()
     sk = [add_relaxed(nk, pat, g, 0, reverse=True) for g, (_t, pat, _a) in enumerate(rules.kw_groups) if pat]
     if not sk:                       # no keywords: a one-state automaton that never accepts
         sk = [add_relaxed(nk, "\\xff\\x00\\xff", 0, 0, reverse=True)]
     scan_k = build_mealy_dfa(nk, sk)
-    if scan_d.n_classes + 1 > 255 or scan_k.n_classes + 1 > 255:
+    groups = plan_scan_groups(rules, scan_budget, _table_bytes(scan_k))
+    scan_d = groups[0][1]
+    for _, m in groups:
+        if m.n_classes + 1 > 255:
+            raise RuleError("too many byte classes")
+    if scan_k.n_classes + 1 > 255:
         raise RuleError("too many byte classes")
     cmap2 = scan_d.cmap.astype(np.uint16) | (scan_k.cmap.astype(np.uint16) << 8)
     k_off, k_ids = _acc_tables(scan_k)
@@ -950,8 +1025,23 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
             ne += 1
     if ne > 8:
         raise RuleError("more than 8 excluder patterns")
-    scan_d.acc_sets = [tuple(sorted(s, key=lambda pid: (exidx[pid] == 0xFF, pid))) for s in scan_d.acc_sets]
-    d_off, d_ids = _acc_tables(scan_d)
+    # one accept-set id space over all scan groups: group g's set a > 0 -> acc_base[g] + a
+    acc_sets: List[Tuple[int, ...]] = [()]
+    acc_base = []
+    for _, m in groups:
+        m.acc_sets = [tuple(sorted(s, key=lambda pid: (exidx[pid] == 0xFF, pid))) for s in m.acc_sets]
+        acc_base.append(len(acc_sets) - 1)
+        acc_sets.extend(m.acc_sets[1:])
+    d_off = np.zeros(len(acc_sets) + 1, dtype=np.uint32)
+    d_list: List[int] = []
+    for i, st in enumerate(acc_sets):
+        d_list.extend(st)
+        d_off[i + 1] = len(d_list)
+    d_ids = np.array(d_list or [0], dtype=np.uint16)
+
+    def global_accid(g, m):
+        a = m.acc_id.reshape(-1).astype(np.int64)
+        return np.where(a > 0, a + acc_base[g], 0).astype(np.uint16)
     hot = []
     for hr in hot_rules:
         n3 = NFA()
@@ -988,12 +1078,12 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     meta = np.array([P, G, T, V,
                      scan_d.n_states, scan_d.n_classes + 1, scan_d.start,
                      scan_k.n_states, scan_k.n_classes + 1, scan_k.start,
-                     len(hot_rules), min_len, scan_budget, window_ok, 0, 0], dtype=np.int64)
+                     len(hot_rules), min_len, scan_budget, window_ok, len(groups) - 1, 0], dtype=np.int64)
     S = OrderedDict()
     S["meta"] = meta
     S["scan.cmap2"] = cmap2
     S["scan.d.trans"] = scan_d.trans.reshape(-1)
-    S["scan.d.accid"] = scan_d.acc_id.reshape(-1).astype(np.uint16)
+    S["scan.d.accid"] = global_accid(0, scan_d)
     S["scan.d.acc_off"] = d_off
     S["scan.d.acc_ids"] = d_ids
     S["scan.k.trans"] = scan_k.trans.reshape(-1)
@@ -1019,8 +1109,16 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     S["kw.type"] = kw_type
     S["kw.always"] = kw_always
     S["types.names"] = np.frombuffer(names_blob, dtype=np.uint8).copy()
+    # scan groups >= 1 (config-5 scale): (states, classes + EOT, start) + class map, table, accept ids
+    if len(groups) > 1:
+        S["scan.groups"] = np.array([[m.n_states, m.n_classes + 1, m.start, 0] for _, m in groups[1:]],
+                                    dtype=np.int64).reshape(-1)
+        for g, (_, m) in enumerate(groups[1:], start=1):
+            S[f"scan.g{g}.cmap"] = m.cmap.astype(np.uint8)
+            S[f"scan.g{g}.trans"] = m.trans.reshape(-1)
+            S[f"scan.g{g}.accid"] = global_accid(g, m)
     blob = _sections_to_blob(S)
-    return Compiled(rules, scan_d, scan_k, first, hot, hot_rules, S, blob)
+    return Compiled(rules, scan_d, scan_k, first, hot, hot_rules, S, blob, [[p.pid for p in ps] for ps, _ in groups])
 
 
 def _min_len(tree) -> int:

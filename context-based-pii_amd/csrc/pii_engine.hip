@@ -372,6 +372,7 @@ __global__ __launch_bounds__(256) void k_lane_bits(const RulesDev R, const Geo g
     const uint32_t top = scan_top(g, L);
     if (top <= L.lo) return;
     if (L.chi) lane_st[2 * c] = halo_state(R, g, text, L);
+    if (!words) return;                      // SCAN groups >= 1: only their halo states
     const int64_t b_hi = ((int64_t)top - 1 + g.r0) >> 6, b_lo = ((int64_t)L.lo + g.r0) >> 6;
     const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
     const uint32_t slot = lane_pos[c];
@@ -915,7 +916,18 @@ constexpr int PAIRS_BLOCK = 256;
 // Two launches: WRITE = false counts each lane's pairs (and records the AGENT rows' keyword groups),
 // an exclusive scan of the counts gives every lane its block of the queue (lane order, no atomics),
 // WRITE = true fills the blocks.
-template <bool WRITE>
+//
+// MULTI (a rule set split over several SCAN groups, config 5): every group's k_scan pass wrote its
+// own per-lane event list (descending position, arena g at ev + g * ev_stride); the lists are merged
+// here by position, a tie going to the higher group first so that, the queue being filled back to
+// front, group 0 (built-ins and excluders) comes first among one start's pairs.  Only group 0 steps
+// the keyword automaton.  The count pass also writes each lane's total event count (lane_evn).
+constexpr int SCAN_GROUPS_MAX = 8;
+struct AccTabs {                 // per SCAN group: transition index -> global D accept-set id
+    const uint16_t* accid[SCAN_GROUPS_MAX];
+};
+
+template <bool WRITE, bool MULTI>
 __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const Geo g,
                                                const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
                                                const uint8_t* __restrict__ role, int32_t* __restrict__ kw,
@@ -923,7 +935,9 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
                                                uint64_t pair_cap, uint64_t ev_cap,
                                                const uint64_t* __restrict__ lane_pair,
                                                const uint64_t* __restrict__ lane_ev,
-                                               uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err) {
+                                               uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err,
+                                               uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
+                                               const AccTabs acct, uint32_t* __restrict__ lane_evn) {
     __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
     __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
     __shared__ uint32_t s_acc_off[256];
@@ -958,15 +972,65 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : (int64_t)offs[u] - base; };
     auto uagent = [&](int64_t u) { return (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT; };
 
-    const uint32_t cnt = valid ? lane_cnt[c] : 0u;
-    const Event* evl = nullptr;
+    // the lane's events in descending position: one list, or the merge of the groups' lists
+    uint32_t cnt = 0;
     int64_t u_top = 0;
     Lane L{};
+    uint64_t evoff = 0;
+    if (valid) {
+        if (MULTI) {
+            for (uint32_t q = 0; q < n_groups; ++q) cnt += lane_cnt[(uint64_t)q * cnt_stride + c];
+        } else {
+            cnt = lane_cnt[c];
+        }
+    }
     if (cnt) {
         L = g_lane(g, c);
-        evl = ev + ev_base(L, c);
+        evoff = ev_base(L, c);
         u_top = (int64_t)L.u1 - 1;
     }
+    const Event* evl = ev + evoff;
+    uint32_t k1 = 0;                        // single list: next index
+    Event En = (!MULTI && cnt) ? evl[0] : Event{};
+    uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX];
+    Event gh[SCAN_GROUPS_MAX];
+    if (MULTI) {
+#pragma unroll
+        for (int q = 0; q < SCAN_GROUPS_MAX; ++q) {
+            gk[q] = 0;
+            gn[q] = (cnt && (uint32_t)q < n_groups) ? lane_cnt[(uint64_t)q * cnt_stride + c] : 0u;
+            gh[q] = gn[q] ? evl[(uint64_t)q * ev_stride] : Event{};
+        }
+    }
+    // next event (E) and its D accept set; k0: it is group 0's (the keyword automaton's group)
+    auto next = [&](Event& E, uint32_t& acc, bool& k0) {
+        if (!MULTI) {
+            E = En;
+            if (k1 + 1 < cnt) En = evl[k1 + 1];
+            ++k1;
+            acc = R.d_accid[E.sd];
+            k0 = true;
+            return;
+        }
+        int best = -1;
+        uint32_t bp = 0;
+#pragma unroll
+        for (int q = SCAN_GROUPS_MAX - 1; q >= 0; --q)
+            if (gk[q] < gn[q] && (best < 0 || gh[q].pos > bp)) {
+                best = q;
+                bp = gh[q].pos;
+            }
+#pragma unroll
+        for (int q = 0; q < SCAN_GROUPS_MAX; ++q)
+            if (q == best) {
+                E = gh[q];
+                acc = acct.accid[q][E.sd];
+                ++gk[q];
+                if (gk[q] < gn[q]) gh[q] = evl[(uint64_t)q * ev_stride + gk[q]];
+            }
+        k0 = best == 0;
+    };
+
     if (!WRITE) {
         // count pairs, keyword groups of AGENT rows (a cut row's lanes merge theirs with an atomic min:
         // -1 = no hit is the largest unsigned value)
@@ -982,10 +1046,11 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
         int64_t s_u = cnt ? uoff(u) : 0;
         bool agent = cnt ? uagent(u) : false;
         int grp = KW_NONE;
-        Event En = cnt ? evl[0] : Event{};
         for (uint32_t k = 0; k < cnt; ++k) {
-            const Event E = En;
-            if (k + 1 < cnt) En = evl[k + 1];      // next event in flight while this one decodes
+            Event E;
+            uint32_t acc;
+            bool k0;
+            next(E, acc, k0);
             const int64_t pos = E.pos;
             while (pos < s_u) {
                 if (grp != KW_NONE) put_kw(u, grp);
@@ -994,15 +1059,17 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
                 s_u = uoff(u);
                 agent = uagent(u);
             }
-            const uint32_t acc = R.d_accid[E.sd];
             np += acc_off(acc + 1) - acc_off(acc);
-            if (agent) {
+            if (agent && k0) {
                 const uint32_t a = R.k_accid[E.sk];
                 if (a) grp = min(grp, (int)kmin(a));
             }
         }
         if (cnt && grp != KW_NONE) put_kw(u, grp);
-        if (valid) lane_np[c] = np;
+        if (valid) {
+            lane_np[c] = np;
+            if (MULTI) lane_evn[c] = cnt;
+        }
         return;
     }
     if (!valid) return;
@@ -1019,17 +1086,17 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     int64_t u = u_top;
     int64_t s_u = uoff(u);
     int64_t e_u = uoff(u + 1);
-    Event En = evl[0];
     for (uint32_t k = 0; k < cnt; ++k) {
-        const Event E = En;
-        if (k + 1 < cnt) En = evl[k + 1];
+        Event E;
+        uint32_t acc;
+        bool k0;
+        next(E, acc, k0);
         const int64_t pos = E.pos;
         while (pos < s_u) {
             --u;
             e_u = s_u;
             s_u = uoff(u);
         }
-        const uint32_t acc = R.d_accid[E.sd];
         const uint32_t a0 = acc_off(acc), a1 = acc_off(acc + 1);
         w -= a1 - a0;
         EvPairs ep;
@@ -1102,7 +1169,11 @@ __global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs*
     }
 }
 
+// GI: the image is too large for LDS (config-5 rule sets: every FIRST automaton of 500+ types) and
+// is read in place from global memory (L2-resident), the kernel launched without dynamic LDS
+template <bool GI = false>
 __device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ img, uint32_t total, uint4* lds4) {
+    if (GI) return reinterpret_cast<const uint8_t*>(img);
     for (uint32_t i = threadIdx.x; i < total / 16; i += blockDim.x) lds4[i] = img[i];
     __syncthreads();
     return reinterpret_cast<const uint8_t*>(lds4);
@@ -1113,6 +1184,7 @@ __device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ i
 // segment of `matched` and the runs still alive after one 16-byte window into the same segment of
 // `cont`.  The workgroup then finishes all its continuations densely, so one long run no longer holds
 // 63 idle lanes; their matches are appended through LDS counters.
+template <bool GI>
 __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
                                                            const uint8_t* __restrict__ text0,
                                                            const uint64_t* __restrict__ offs,
@@ -1129,7 +1201,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restri
         if (threadIdx.x < PAIR_WAVES) mcount[blockIdx.x * PAIR_WAVES + threadIdx.x] = 0;
         return;
     }
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[FI_TRANS]), lb + li.off[FI_CMAP]};
     const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + li.off[FI_DESC]);
     const uint64_t n = min((uint64_t)*pair_count, pair_cap);
@@ -1199,6 +1271,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restri
 }
 
 // per matched pair: validator + hotword windows of the row's context variant -> likelihood
+template <bool GI>
 __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
                                                           const uint8_t* __restrict__ text0,
                                                           const uint64_t* __restrict__ offs,
@@ -1211,7 +1284,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
                                                           const int32_t* __restrict__ pend,
                                                           PairRes* __restrict__ pres) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
     const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
@@ -1553,11 +1626,12 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     }
 }
 
+template <bool GI>
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 const Geo g, const SelIO io, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & ERR_ABORT) return;           // the batch is re-run with a larger queue
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= g.n_chunks) return;
@@ -1617,13 +1691,14 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint
 }
 
 // re-run every maximal chain of dirty lanes from the clean lane before it (one thread per chain)
+template <bool GI>
 __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                  const Geo g, const SelIO io, const uint32_t* __restrict__ long_rows,
                                                  const uint32_t* __restrict__ long_count,
                                                  const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & ERR_ABORT) return;
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         uint32_t ca, kb;
@@ -3007,9 +3082,12 @@ bool parse_blob(const uint8_t* p, size_t n, std::vector<Section>& out) {
 }  // namespace
 
 // ================================================================================ engine object
+constexpr size_t IMG_LDS_MAX = 160 * 1024;
 struct DevImage {
     LdsImage li{};
     uint4* d = nullptr;
+    bool global = false;      // larger than LDS: kernels read it in place (load_image<true>)
+    size_t lds() const { return global ? 0 : li.total; }
 };
 
 // packs `parts` (16-byte aligned sections) into one image and uploads it
@@ -3022,7 +3100,7 @@ static bool make_image(const std::vector<std::pair<const void*, size_t>>& parts,
     }
     if (off == 0) off = 16;
     out.li.total = (uint32_t)off;
-    if (off > 160 * 1024) return false;
+    out.global = off > IMG_LDS_MAX;
     std::vector<uint8_t> img(off, 0);
     for (size_t i = 0; i < parts.size(); ++i)
         if (parts[i].second) std::memcpy(img.data() + out.li.off[i], parts[i].first, parts[i].second);
@@ -3042,7 +3120,14 @@ struct pii_engine {
     uint32_t n_slots = 0;
     int64_t ttl_us = 0;
     size_t scan_lds = 0;
+    // SCAN groups (config-5 scale rule sets: one reverse D automaton per k_scan pass; sg[0] = R)
+    uint32_t n_sg = 1;
+    std::vector<RulesDev> sg;
+    std::vector<size_t> sg_lds;
+    AccTabs acct{};
+    uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs<.., MULTI>)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
+    bool wsel_ok = true;               // the window re-scan's images fit in LDS
     int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
@@ -3196,9 +3281,9 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
     // event arenas: a lane's emitted positions + its utterance starts (ev_base); findings arenas:
     // one finding per min_len bytes + one per lane (fd_base)
     const uint64_t need_ev = bytes + n_utt + n_lanes + 2, need_fd = bytes / e->R.min_len + n_lanes + 2;
-    if (need_ev > e->cap_ev) {
+    if (need_ev > e->cap_ev) {           // one arena per SCAN group, cap_ev events apart
         const uint64_t nb = std::max<uint64_t>(need_ev + need_ev / 8, 1 << 16);
-        if ((rc = grow(e, e->ev, nb))) return rc;
+        if ((rc = grow(e, e->ev, nb * e->n_sg))) return rc;
         e->cap_ev = nb;
     }
     if (need_fd > e->cap_fd) {
@@ -3213,12 +3298,13 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         if ((rc = grow(e, e->lane_perm, nl))) return rc;
         if ((rc = grow(e, e->lane_pos, nl))) return rc;
         if ((rc = grow(e, e->lane_bkt, 2 * LANE_NB))) return rc;
-        if ((rc = grow(e, e->lane_cnt, nl))) return rc;
+        if ((rc = grow(e, e->lane_cnt, nl * e->n_sg))) return rc;
+        if (e->n_sg > 1 && (rc = grow(e, e->lane_evn, nl))) return rc;
         if ((rc = grow(e, e->lane_ev, nl))) return rc;
         if ((rc = grow(e, e->bnd, nl * LANE_WORDS))) return rc;
         if ((rc = grow(e, e->lane_pair, nl))) return rc;
         if ((rc = grow(e, e->lane_np, nl))) return rc;
-        if ((rc = grow(e, e->lane_st, 2 * nl))) return rc;
+        if ((rc = grow(e, e->lane_st, 2 * nl * e->n_sg))) return rc;
         if ((rc = grow(e, e->lane_nf, nl))) return rc;
         if ((rc = grow(e, e->lane_rd, nl))) return rc;
         if ((rc = grow(e, e->lane_reach, nl))) return rc;
@@ -3375,25 +3461,50 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
             k_lane_count<<<nsb, 256, 0, st>>>(g, e->lane_bkt);
             k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
-            k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(R, g, text, e->lane_pos, e->bnd, e->lane_st);
-            HIPCHK(hipEventRecord(e->kev[0], st));
-            k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->scan_lds, st>>>(
-                R, g, text, e->bnd, e->lane_perm, e->ev, e->lane_cnt, e->lane_st, e->d_err);
-            HIPCHK(hipEventRecord(e->kev[1], st));
-            if (e->long_min != NO_CUTS)
-                k_scan_fix<<<row_grid(e, total_bytes), 256, e->scan_lds + FIX_LDS, st>>>(
-                    R, g, text, e->long_rows, e->long_count, e->ev, e->lane_cnt, e->lane_st, (uint32_t)e->scan_lds,
-                    e->d_err);
+            // one pass per SCAN group (one for the shipped rules): halo states, scan, stitching; the
+            // utterance-start words are written once
+            for (uint32_t q = 0; q < e->n_sg; ++q) {
+                const RulesDev& Rq = e->sg[q];
+                Event* evq = e->ev + (uint64_t)q * e->cap_ev;
+                uint32_t* cq = e->lane_cnt + (uint64_t)q * e->cap_lanes;
+                uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
+                k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(Rq, g, text, e->lane_pos,
+                                                                     q == 0 ? e->bnd : nullptr, stq);
+                if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
+                k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->sg_lds[q], st>>>(
+                    Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
+                if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
+                if (e->long_min != NO_CUTS)
+                    k_scan_fix<<<row_grid(e, total_bytes), 256, e->sg_lds[q] + FIX_LDS, st>>>(
+                        Rq, g, text, e->long_rows, e->long_count, evq, cq, stq, (uint32_t)e->sg_lds[q], e->d_err);
+            }
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
-            k_pairs<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc, e->evpairs,
-                                                        e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev, e->lane_np,
-                                                        e->d_err);
+            const bool multi = e->n_sg > 1;
+            const uint32_t ns = e->n_sg, cs = (uint32_t)e->cap_lanes;
+            const uint64_t es = e->cap_ev;
+            if (multi)
+                k_pairs<false, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
+                                                                  e->lane_evn);
+            else
+                k_pairs<false, false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                   e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                   e->lane_ev, e->lane_np, e->d_err, ns, es, cs,
+                                                                   e->acct, nullptr);
             int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
-            if ((rc = exclusive_scan(e, e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
-            k_pairs<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc, e->evpairs,
-                                                       e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev, e->lane_np,
-                                                       e->d_err);
+            if ((rc = exclusive_scan(e, multi ? e->lane_evn : e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
+            if (multi)
+                k_pairs<true, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                 e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
+                                                                 e->lane_evn);
+            else
+                k_pairs<true, false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs,
+                                                                  e->acct, nullptr);
             k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
         }
         HIPCHK(hipGetLastError());
@@ -3410,7 +3521,8 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
     if (n_utt > 0 && n_chunks > 0) {
-        k_pair_first<<<e->n_seg, PAIR_BLOCK, e->img_first.li.total, st>>>(
+        (e->img_first.global ? k_pair_first<true> : k_pair_first<false>)<<<e->n_seg, PAIR_BLOCK,
+                                                                            e->img_first.lds(), st>>>(
             e->img_first.d, e->img_first.li, text, offs, pcount, e->pair_cap, e->evloc, e->pres, e->pend, e->matched,
             e->cont, e->mcount, e->d_err);
         HIPCHK(hipGetLastError());
@@ -3447,17 +3559,18 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                            st)))
         return rc;
     if (n_utt > 0 && n_chunks > 0) {
-        k_pair_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
+        (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
+                                                                         st>>>(
             e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
             e->mcount, e->n_seg, e->evloc, e->pend, e->pres);
         const SelIO io{e->lane_pair, e->lane_np, e->evloc, e->pres, e->pend, e->pair_cap, role, ctx, e->fd,
                        e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill};
-        k_select<<<(n_chunks + 255) / 256, 256, e->img_sel.li.total, st>>>(R, e->img_sel.d, e->img_sel.li, g, io,
-                                                                          e->d_err);
+        (e->img_sel.global ? k_select<true> : k_select<false>)<<<(n_chunks + 255) / 256, 256, e->img_sel.lds(), st>>>(
+            R, e->img_sel.d, e->img_sel.li, g, io, e->d_err);
         const uint32_t rg = row_grid(e, total_bytes);
         k_sel_dirty<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_reach, e->dirty, e->d_err);
-        k_sel_fix<<<rg, 256, e->img_sel.li.total, st>>>(R, e->img_sel.d, e->img_sel.li, g, io, e->long_rows,
-                                                        e->long_count, e->dirty, e->d_err);
+        (e->img_sel.global ? k_sel_fix<true> : k_sel_fix<false>)<<<rg, 256, e->img_sel.lds(), st>>>(
+            R, e->img_sel.d, e->img_sel.li, g, io, e->long_rows, e->long_count, e->dirty, e->d_err);
         k_rowlen<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_rd, e->lane_rowbase, e->out_len,
                                           e->d_err);
         HIPCHK(hipGetLastError());
@@ -3685,20 +3798,20 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     }
     // host-side derived tables
     std::vector<uint16_t> td(R.SD * R.CDs, 0), tk(R.SK * R.CKs, 0), dacc(R.SD * R.CDs, 0), kacc(R.SK * R.CKs, 0);
+    // entry (row, class) = address of the destination row | accept | accept of the destination's
+    // end-of-text transition (class C-1) << 1, so k_scan resets at an utterance start without
+    // reading the end-of-text entry
+    auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, uint32_t base,
+                       uint16_t* t, uint16_t* a) {
+        for (int r = 0; r < S; ++r)
+            for (int c = 0; c < C; ++c) {
+                const uint32_t v = s[r * C + c], dst = v & 0x7fff;
+                const uint32_t eot = s[dst * C + C - 1] >> 15;
+                t[r * Cs + c] = (uint16_t)((base + dst * Cs * 2) | (v >> 15) | (eot << 1));
+                a[r * Cs + c] = acc[r * C + c];
+            }
+    };
     {
-        // entry (row, class) = address of the destination row | accept | accept of the destination's
-        // end-of-text transition (class C-1) << 1, so k_scan resets at an utterance start without
-        // reading the end-of-text entry
-        auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, uint32_t base,
-                           uint16_t* t, uint16_t* a) {
-            for (int r = 0; r < S; ++r)
-                for (int c = 0; c < C; ++c) {
-                    const uint32_t v = s[r * C + c], dst = v & 0x7fff;
-                    const uint32_t eot = s[dst * C + C - 1] >> 15;
-                    t[r * Cs + c] = (uint16_t)((base + dst * Cs * 2) | (v >> 15) | (eot << 1));
-                    a[r * Cs + c] = acc[r * C + c];
-                }
-        };
         relayout(reinterpret_cast<const uint16_t*>(find("scan.d.trans")->data),
                  reinterpret_cast<const uint16_t*>(find("scan.d.accid")->data), R.SD, R.CD, R.CDs, SCAN_TD_BASE,
                  td.data(), dacc.data());
@@ -3753,6 +3866,45 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     tok += "\n";               // the re-scan window separator (k_win_redact piece source)
     R.nl_off = (uint32_t)tok.size() - 1;
     tok.append(32, '\0');     // k_redact reads aligned 16-byte windows past a token's end
+    // SCAN groups >= 1: their own D automaton and class map, a 1-row never-accepting K stub
+    struct HostGroup {
+        int SD, CD, CDs, start;
+        uint32_t lds;
+        std::vector<uint16_t> td, tk, dacc, kacc;
+        std::vector<uint32_t> cmap4;
+    };
+    std::vector<HostGroup> hg;
+    {
+        const int64_t n_extra = meta[14];
+        if (n_extra < 0 || n_extra + 1 > SCAN_GROUPS_MAX) return fail("too many SCAN groups");
+        const Section* gs = find("scan.groups");
+        if (n_extra > 0 && (!gs || gs->bytes < (size_t)n_extra * 32)) return fail("SCAN group table missing");
+        for (int64_t q = 1; q <= n_extra; ++q) {
+            const int64_t* gm = reinterpret_cast<const int64_t*>(gs->data) + 4 * (q - 1);
+            const std::string nm = "scan.g" + std::to_string(q);
+            const Section *sc = find((nm + ".cmap").c_str()), *st = find((nm + ".trans").c_str()),
+                          *sa = find((nm + ".accid").c_str());
+            HostGroup h;
+            h.SD = (int)gm[0];
+            h.CD = (int)gm[1];
+            h.CDs = (h.CD + 1) & ~1;
+            if (!sc || !st || !sa || st->bytes != (size_t)h.SD * h.CD * 2 || sa->bytes != st->bytes || sc->bytes != 256)
+                return fail("SCAN group tables malformed");
+            const uint32_t tkb = SCAN_TD_BASE + (uint32_t)(h.SD * h.CDs) * 2;
+            h.lds = tkb + 4;                                    // + the K stub's row (2 entries)
+            if (h.lds > 65536) return fail("a SCAN group exceeds 64 KiB of LDS");
+            h.td.assign((size_t)h.SD * h.CDs, 0);
+            h.dacc.assign((size_t)h.SD * h.CDs, 0);
+            relayout(reinterpret_cast<const uint16_t*>(st->data), reinterpret_cast<const uint16_t*>(sa->data), h.SD,
+                     h.CD, h.CDs, SCAN_TD_BASE, h.td.data(), h.dacc.data());
+            h.tk = {(uint16_t)tkb, (uint16_t)tkb};
+            h.kacc = {0, 0};
+            h.start = (int)(SCAN_TD_BASE + gm[2] * h.CDs * 2);
+            h.cmap4.resize(256);
+            for (int b = 0; b < 256; ++b) h.cmap4[b] = 2u * sc->data[b];        // K stub: class 0
+            hg.push_back(std::move(h));
+        }
+    }
     // one device buffer holding every table, 256-byte aligned sections
     struct Put {
         const void* src;
@@ -3777,6 +3929,11 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
            i_ro = addsec("var.rule_off"), i_ri = addsec("var.rule_ids"), i_eo = addsec("var.excl_off"),
            i_ei = addsec("var.excl_ids"), i_to = add(tok_off.data(), tok_off.size() * 4),
            i_tb = add(tok.data(), tok.size());
+    struct GroupPut { size_t cmap, td, tk, dacc, kacc; };
+    std::vector<GroupPut> gp;
+    for (auto& h : hg)
+        gp.push_back({add(h.cmap4.data(), 1024), add(h.td.data(), h.td.size() * 2), add(h.tk.data(), 4),
+                      add(h.dacc.data(), h.dacc.size() * 2), add(h.kacc.data(), 4)});
     if (hipSetDevice(device) != hipSuccess) { e->err = "hipSetDevice failed"; pii_engine_destroy(e); return PII_E_DEVICE; }
     if (hipMalloc(&e->d_rules, total) != hipSuccess) return fail("hipMalloc rules failed");
     std::vector<uint8_t> host(total, 0);
@@ -3807,6 +3964,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.excl_ids = (const uint16_t*)at(i_ei);
     R.tok_off = (const uint32_t*)at(i_to);
     R.tok_bytes = (const uint8_t*)at(i_tb);
+    if (R.n_dacc >= 65535) return fail("too many SCAN accept sets");
     {   // per-kernel LDS images
         auto sec = [&](const char* nm) { return std::make_pair((const void*)find(nm)->data, (size_t)find(nm)->bytes); };
         const uint16_t* ptrans = (const uint16_t*)find("pool.trans")->data;
@@ -3860,7 +4018,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         pw[WS_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         pw[WS_ROFF] = sec("var.rule_off");
         pw[WS_RIDS] = sec("var.rule_ids");
-        if (!make_image(pw, e->img_wsel)) return fail("rule tables do not fit in LDS / upload failed");
+        if (!make_image(pw, e->img_wsel)) return fail("rule table upload failed");
         ps[SE_DTYPE] = sec("det.type");
         ps[SE_VEN] = sec("var.enabled");
         ps[SE_VMIN] = sec("var.minlik");
@@ -3869,14 +4027,16 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         ps[SE_XIDS] = sec("var.excl_ids");
         ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
-            return fail("rule tables do not fit in LDS / upload failed");
+            return fail("rule table upload failed");
+        // the window re-scan keeps its tables in LDS (rule sets whose images do not fit cannot enable it)
+        e->wsel_ok = !e->img_wsel.global && !e->img_eval.global;
         const std::pair<const void*, const DevImage*> big[] = {
-            {(const void*)k_pair_first, &e->img_first}, {(const void*)k_pair_eval, &e->img_eval},
-            {(const void*)k_select, &e->img_sel}, {(const void*)k_sel_fix, &e->img_sel},
+            {(const void*)k_pair_first<false>, &e->img_first}, {(const void*)k_pair_eval<false>, &e->img_eval},
+            {(const void*)k_select<false>, &e->img_sel}, {(const void*)k_sel_fix<false>, &e->img_sel},
             {(const void*)k_win_eval, &e->img_eval},
             {(const void*)k_win_select, &e->img_wsel}, {(const void*)k_win_halo, &e->img_eval}};
         for (auto& kb : big)
-            if (kb.second->li.total > 64 * 1024 &&
+            if (!kb.second->global && kb.second->li.total > 64 * 1024 &&
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
                     hipSuccess)
                 return fail("cannot raise the LDS limit of a pair kernel");
@@ -3888,12 +4048,37 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     }
     e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
-    if (e->scan_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->scan_lds) != hipSuccess)
+    e->n_sg = 1 + (uint32_t)hg.size();
+    e->sg.assign(1, R);
+    e->sg_lds.assign(1, e->scan_lds);
+    e->acct.accid[0] = R.d_accid;
+    for (size_t q = 0; q < hg.size(); ++q) {
+        RulesDev Rq = R;
+        const HostGroup& h = hg[q];
+        Rq.cmap4 = (const uint32_t*)at(gp[q].cmap);
+        Rq.td = (const uint16_t*)at(gp[q].td);
+        Rq.tk = (const uint16_t*)at(gp[q].tk);
+        Rq.d_accid = (const uint16_t*)at(gp[q].dacc);
+        Rq.k_accid = (const uint16_t*)at(gp[q].kacc);
+        Rq.SD = h.SD;
+        Rq.CD = h.CD;
+        Rq.CDs = h.CDs;
+        Rq.d_start = h.start;
+        Rq.SK = 1;
+        Rq.CK = 2;
+        Rq.CKs = 2;
+        Rq.k_start = (int)(h.lds - 4);
+        e->sg.push_back(Rq);
+        e->sg_lds.push_back(h.lds);
+        e->acct.accid[q + 1] = Rq.d_accid;
+    }
+    const size_t max_lds = *std::max_element(e->sg_lds.begin(), e->sg_lds.end());
+    if (max_lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) != hipSuccess)
         return fail("cannot raise LDS limit");
-    if (e->scan_lds + FIX_LDS > 64 * 1024 &&
+    if (max_lds + FIX_LDS > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(e->scan_lds + FIX_LDS)) != hipSuccess)
+                            (int)(max_lds + FIX_LDS)) != hipSuccess)
         return fail("cannot raise LDS limit");
     e->hist_types = (uint32_t)std::min(R.T, 1024);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
@@ -3932,7 +4117,7 @@ int pii_engine_destroy(pii_engine* e) {
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
-                    e->long_rows, e->long_count, e->lane_st, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
+                    e->long_rows, e->long_count, e->lane_st, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
                     e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -4213,8 +4398,9 @@ int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
         e->err = "a detector can match '\\n' or a text edge: windows cannot be re-scanned incrementally";
         return PII_E_RULES;
     }
-    if (e->R.P > P_MAX) {
-        e->err = "the window re-scan keeps per-pattern state for at most P_MAX detector patterns";
+    if (e->R.P > P_MAX || e->n_sg > 1 || !e->wsel_ok) {
+        e->err = "the window re-scan needs a rule set of at most P_MAX detector patterns, one SCAN group and "
+                 "LDS-resident tables";
         return PII_E_RULES;
     }
     HIPCHK(hipSetDevice(e->device));

@@ -54,6 +54,14 @@ class TableSim:
         from oracle import pii_oracle as O
         self.validators = [None, O.v_luhn, O.v_nanp, O.v_ssn, O.v_ein, O.v_ipv4, O.v_swift, O.v_iban]
         self.excluder_types = set(int(x) for x in self.excl_ids[:int(self.excl_off[-1])])
+        # scan groups >= 1 (config-5 scale): D automata without K, one engine k_scan pass each
+        self.groups = []
+        if "scan.groups" in S:
+            gm = S["scan.groups"].reshape(-1, 4)
+            for g in range(1, len(gm) + 1):
+                ns, nc, st = int(gm[g - 1][0]), int(gm[g - 1][1]), int(gm[g - 1][2])
+                self.groups.append((S[f"scan.g{g}.cmap"], S[f"scan.g{g}.trans"].reshape(ns, nc),
+                                    S[f"scan.g{g}.accid"].reshape(ns, nc), st, nc))
 
     # ---------------------------------------------------------------- K1: reverse scan
     def scan(self, text: bytes, agent: bool) -> List[Tuple[int, int, int]]:
@@ -70,7 +78,27 @@ class TableSim:
         nk = int(self.tk[sk, self.CK - 1])
         if (nd & 0x8000) or (agent and (nk & 0x8000)):
             ev.append((0, sd, sk))
+        # groups >= 1: D events only; sd carries the group (g << 20), sk = -1
+        for g, (cm, td, _acc, st, nc) in enumerate(self.groups, start=1):
+            sd = st
+            for j in range(len(text) - 1, -1, -1):
+                nd = int(td[sd, int(cm[text[j]])])
+                if nd & 0x8000:
+                    ev.append((j + 1, (g << 20) | sd, -1))
+                sd = nd & 0x7FFF
+            if int(td[sd, nc - 1]) & 0x8000:
+                ev.append((0, (g << 20) | sd, -1))
         return ev
+
+    def d_accept(self, text: bytes, pos: int, sd: int) -> int:
+        """global accept-set id of a D event (any scan group)"""
+        g = sd >> 20
+        if g == 0:
+            cd, _ = self._classes(text, pos)
+            return int(self.dacc[sd, cd])
+        cm, _td, acc, _st, nc = self.groups[g - 1]
+        c = nc - 1 if pos == 0 else int(cm[text[pos - 1]])
+        return int(acc[sd & 0xFFFFF, c])
 
     def _classes(self, text, pos):
         if pos == 0:
@@ -82,6 +110,8 @@ class TableSim:
     def keyword_group(self, text: bytes, events) -> int:
         best = min([g for g in range(self.G) if self.kw_always[g]] or [1 << 30])
         for pos, sd, sk in events:
+            if sk < 0:
+                continue
             _, ck = self._classes(text, pos)
             a = int(self.kacc[sk, ck])
             for i in range(int(self.k_off[a]), int(self.k_off[a + 1])):
@@ -121,12 +151,14 @@ class TableSim:
         last_ex = {}
         kept, max_end = [], -1
         minlik = int(self.minlik[v])
-        for pos, sd, sk in sorted(events):
-            cd, _ = self._classes(text, pos)
-            a = int(self.dacc[sd, cd])
+        by_pos = {}
+        for pos, sd, sk in sorted(events):          # one start: every group's accept set, group 0 first
+            a = self.d_accept(text, pos, sd)
+            by_pos.setdefault(pos, []).extend(int(self.d_ids[i]) for i in range(int(self.d_off[a]),
+                                                                                int(self.d_off[a + 1])))
+        for pos in sorted(by_pos):
             at_s = []
-            for i in range(int(self.d_off[a]), int(self.d_off[a + 1])):
-                p = int(self.d_ids[i])
+            for p in by_pos[pos]:
                 t = int(self.det_type[p])
                 if not self.enabled[v, t] or pos < cur[p]:
                     continue
@@ -202,8 +234,7 @@ class TableSim:
         W = b"\n".join(list(preds) + [text])
         oj = len(W) - len(text)
         for pos, sd, sk in sorted(events):
-            cd, _ = self._classes(text, pos)
-            a = int(self.dacc[sd, cd])
+            a = self.d_accept(text, pos, sd)
             for i in range(int(self.d_off[a]), int(self.d_off[a + 1])):
                 p = int(self.d_ids[i])
                 if pos < cur[p]:
