@@ -36,7 +36,7 @@ using namespace pii;
 namespace {
 
 constexpr int P_MAX = 64;          // detector patterns handled by k_select's private state
-constexpr int NE_MAX = 4;          // excluder patterns
+constexpr int NE_MAX = 2;          // excluder patterns
 constexpr int SCAN_BLOCK = 512;
 constexpr int CTX_BLOCK = 1024;
 constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
     }
 }
 
-constexpr int LIVE = 8;            // register-resident "previous match end" slots per lane
+constexpr int LIVE = 5;            // register-resident "previous match end" slots per lane
 
 // bit j: entry g0 + j of an aligned 16-entry pend[] group is a match (>= 0) inside the lane's run
 // [off0, off0 + np)
@@ -1359,6 +1359,18 @@ __device__ __forceinline__ uint32_t matched_mask16(int4 c0, int4 c1, int4 c2, in
     for (int j = 0; j < 16; ++j) m |= (uint32_t)(v[j] >= 0) << j;
     if (g0 < off0) m &= 0xffffu << off0;
     if (g0 + 16u > off0 + np) m &= (1u << (off0 + np - g0)) - 1u;
+    return m;
+}
+
+// bit j: entry g0 + j of an aligned 8-entry pend[] group is a match (>= 0) inside the lane's run
+// [off0, off0 + np)
+__device__ __forceinline__ uint32_t matched_mask8(int4 c0, int4 c1, uint32_t g0, uint32_t off0, uint32_t np) {
+    const int32_t v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m |= (uint32_t)(v[j] >= 0) << j;
+    if (g0 < off0) m &= 0xffu << off0;
+    if (g0 + 8u > off0 + np) m &= (1u << (off0 + np - g0)) - 1u;
     return m;
 }
 
@@ -1455,12 +1467,13 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             fdl[nfl++] = f;
             max_end = best_e;
             const int d = (int)(Tb.tokoff[best_t + 1] - Tb.tokoff[best_t]) - (best_e - s);
-            if (cut_lo_row(u)) rdx += d;
-            else if (cut_row(u)) rdy += d;
-            else {
-                delta_u += d;
-                ++nf_u;
-            }
+            // (selects, not branches: a branch on which counter to add to makes the compiler keep
+            // the counters in a scratch array)
+            const bool clo_r = cut_lo_row(u), cut_r = cut_row(u);
+            rdx += clo_r ? d : 0;
+            rdy += (cut_r && !clo_r) ? d : 0;
+            delta_u += cut_r ? 0 : d;
+            nf_u += cut_r ? 0u : 1u;
         }
         best_e = -1;
     };
@@ -1584,26 +1597,25 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
         const uint32_t np = io.lane_np[lane];
         const uint64_t pbase = io.lane_pair[lane];
         if (np && pbase + np <= io.pair_cap) {
-            // pend[] (4 B per pair, the lane's run) is read 16 entries per iteration as four aligned
+            // pend[] (4 B per pair, the lane's run) is read 8 entries per iteration as two aligned
             // 16-byte loads, the next group issued before this one is decoded; only matched pairs
             // (e >= 0, a small fraction) enter the body.  pend is allocated 16 entries past pair_cap,
             // so the aligned groups never leave the allocation; entries outside the run are masked off.
+            // (8, not 16, entries per group, LIVE = 5 and NE_MAX = 2 keep k_select at 5 waves/SIMD)
             const int32_t* el = io.pend + pbase;
             const uint32_t off0 = (uint32_t)(pbase & 3u);
             const int4* pa = reinterpret_cast<const int4*>(io.pend + (pbase - off0));
-            const uint32_t ng = (off0 + np + 15u) >> 4;
-            int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
+            const uint32_t ng = (off0 + np + 7u) >> 3;
+            int4 q0 = pa[0], q1 = pa[1];
             for (uint32_t gi = 0; gi < ng; ++gi) {
-                const int4 d0 = q0, d1 = q1, d2 = q2, d3 = q3;
+                const int4 d0 = q0, d1 = q1;
                 if (gi + 1 < ng) {
-                    const int4* pn = pa + 4 * (gi + 1);
+                    const int4* pn = pa + 2 * (gi + 1);
                     q0 = pn[0];
                     q1 = pn[1];
-                    q2 = pn[2];
-                    q3 = pn[3];
                 }
-                const uint32_t g0 = 16u * gi;
-                uint32_t m = matched_mask16(d0, d1, d2, d3, g0, off0, np);
+                const uint32_t g0 = 8u * gi;
+                uint32_t m = matched_mask8(d0, d1, g0, off0, np);
                 while (m) {
                     const uint32_t j = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;

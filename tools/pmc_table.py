@@ -11,7 +11,7 @@ d = sys.argv[1]
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = lambda cs, c: sum(cs.get(c, [0])) / max(1, len(cs.get(c, [0])))
 print(f"{'kernel':22s} {'fetchMB':>8s} {'writeMB':>8s} {'VALU_M':>7s} {'LDS_M':>6s} {'VMRD_M':>6s} "
