@@ -337,11 +337,13 @@ def main():
     ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5"], default="scan",
+    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5", "ner"], default="scan",
                     help="scan = config 2 (headline); window = config 3 multi-turn re-scan; "
                          "stream = config 4 PCIe-inclusive batch stream; long = config-2 bytes as long rows; "
                          "config5 = 500+ custom regex / dictionary infoTypes")
     ap.add_argument("--row-kb", type=int, default=1024, help="(long) row size, KiB")
+    ap.add_argument("--ner-batch", type=int, default=64, help="(ner) sequences per step")
+    ap.add_argument("--ner-seq", type=int, default=128, help="(ner) tokens per sequence")
     ap.add_argument("--window-n", type=int, default=5)
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
     ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
@@ -353,6 +355,8 @@ def main():
         return stream_main(args)
     if args.workload == "config5":
         return config5_main(args)
+    if args.workload == "ner":
+        return ner_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
 
@@ -380,6 +384,87 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- config 5: NER on MFMA
+MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 (MI355X_MICROARCH.md; the 2:1-sparse figure is not used)
+
+
+def ner_main(args):
+    """BASELINE config 5's optional NER: bf16 BERT-base token classification (ner.py / csrc/ner.hip)
+    over a batch of --ner-batch sequences x --ner-seq tokens.  value = tokens/s of the whole forward;
+    roofline = the MFMA GEMM (k_gemm) alone, timed with HIP events on the stream it runs on, against
+    the dense bf16 peak.  cpu_baseline = the same HF model in fp32 on the host's CPU share."""
+    import torch
+    N = importlib.import_module("context-based-pii_amd.ner")
+    B, S = args.ner_batch, args.ner_seq
+    cpu = None
+    ref = N.reference_model(seed=0)
+    rng = np.random.default_rng(1)
+    ids = rng.integers(1000, 30522, size=(B, S)).astype(np.int32)
+    ids[:, 0], ids[:, -1] = N.CLS, N.SEP
+    mask = np.ones((B, S), dtype=np.int32)
+    if not args.no_cpu_baseline:
+        cores = cpu_share()
+        torch.set_num_threads(cores)
+        nb = max(1, min(B, 8))
+        with torch.no_grad():
+            ref(input_ids=torch.as_tensor(ids[:1], dtype=torch.long))
+            t0 = time.perf_counter()
+            ref(input_ids=torch.as_tensor(ids[:nb], dtype=torch.long),
+                attention_mask=torch.as_tensor(mask[:nb], dtype=torch.long))
+            dt = time.perf_counter() - t0
+        cpu = {"value": round(nb * S / dt, 1), "unit": "tokens/s", "cores": cores, "kind": "reference",
+               "host_cpu": host_cpu_model(),
+               "sample": f"HF transformers BertForTokenClassification(BertConfig()) fp32 forward, {nb} x {S} tokens, "
+                         f"torch.set_num_threads({cores}), wall {dt:.2f}s"}
+    torch.cuda.set_device(0)
+    m = N.BertNer(ref, device=0)
+    dev = m.dev
+    d_ids, d_mask = torch.as_tensor(ids).to(dev), torch.as_tensor(mask).to(dev)
+    for _ in range(args.warmup):
+        m.forward(d_ids, d_mask)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.forward(d_ids, d_mask)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tokens = B * S
+    # k_gemm alone: one layer's four GEMMs, HIP events on the current stream (where the kernels run)
+    Mp = (tokens + 127) // 128 * 128
+    bu = m._buffers(Mp)
+    Ly = m.layers[0]
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record(st)
+    for _ in range(reps):
+        m.gemm(bu["h"], Ly["wqkv"], Ly["bqkv"], bu["qkv"])
+        m.gemm(bu["ctx"], Ly["wo"], Ly["bo"], bu["a"], N.EPI_RESID, resid=bu["h"])
+        m.gemm(bu["h1"], Ly["wi"], Ly["bi"], bu["f"], N.EPI_GELU)
+        m.gemm(bu["f"], Ly["wf"], Ly["bf"], bu["a"], N.EPI_RESID, resid=bu["h1"])
+    e1.record(st)
+    e1.synchronize()
+    g_ms = e0.elapsed_time(e1) / reps
+    H, I = m.H, m.inter
+    g_flop = 2.0 * Mp * (H * 3 * H + H * H + 2 * H * I)
+    g_tf = g_flop / (g_ms / 1e3) / 1e12
+    flop = m.flops_per_token(S) * tokens
+    line = {
+        "metric": "config 5 NER: tokens/s of bf16 BERT-base token classification (MFMA)", "value": round(tokens * args.steps / el, 1),
+        "unit": "tokens/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"BertConfig() (bert-base, 12 layers, hidden 768) seeded random weights, {B} x {S} tokens",
+                   "model": "bert-base token classification (3 labels)", "global_batch": B, "seq_len": S},
+        "tflops_forward": round(flop * args.steps / el / 1e12, 1),
+        "roofline": {"bound": "mfma", "kernel": "k_gemm", "achieved": round(g_tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(g_tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "algorithmic_flop": int(g_flop), "launch_ms": round(g_ms / 4, 4)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
 
 
 # --------------------------------------------------------------------------- config 5: 500+ types
