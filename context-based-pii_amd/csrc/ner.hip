@@ -10,9 +10,8 @@
 //   ner_classify   logits[M, L] = H . Wc^T + bc                                       f32 out
 //
 // ner_gemm is the dense contraction: 128x128 output tiles per 256-thread workgroup, each wavefront a
-// 64x64 quarter as 2x2 v_mfma_f32_32x32x16_bf16 tiles, K staged through LDS in 32-wide slabs (rows
-// padded by 16 B so the 16-byte fragment reads hit 32 distinct banks), the next slab's global loads
-// in flight while the current one is multiplied.  Operands are K-contiguous (activations row-major,
+// 64x64 quarter as 2x2 v_mfma_f32_32x32x16_bf16 tiles, K DMA'd global -> LDS in 64-wide slabs
+// (global_load_lds, XOR-swizzled 16-byte chunks).  Operands are K-contiguous (activations row-major,
 // nn.Linear weights [out, in]), which is exactly the MFMA's A / B lane map: lane l holds
 // A[row l&31][k 8(l>>5) .. +7] and W[col l&31][same k] -- no transposes anywhere.
 #include <hip/hip_runtime.h>
@@ -31,68 +30,73 @@ __device__ __forceinline__ uint16_t f2bf(float f) {      // round to nearest eve
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
-constexpr int GB_M = 128, GB_N = 128, GB_K = 32;
+constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int G_THREADS = 256;
-constexpr int LDS_ROW = GB_K + 8;      // bf16 per LDS row (64 B of data + 16 B pad)
 
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2 };
 
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
 // C = A . W^T + bias (+ epilogue).  A [M, K], W [N, K], C / R [M, N] bf16; bias f32 [N].
-// Requires M % 128 == 0, N % 128 == 0, K % 32 == 0 (the host pads M).
+// Requires M % 128 == 0, N % 128 == 0, K % 64 == 0 (the host pads M).
+//
+// Per 64-wide K step the workgroup DMAs both 128 x 64 operand slabs straight into LDS
+// (global_load_lds, 16 B per lane: no staging registers), then each wavefront runs 4 k-steps of
+// 2 x 2 MFMAs on its 64 x 64 quarter.  LDS rows are 128 B with the 16-byte chunks XOR-swizzled by
+// (row & 7) -- chunk c of row r is stored at position c ^ (r & 7) -- so the fragment reads of 8
+// consecutive rows (one ds_read_b128 lane group) hit 8 different 16-byte bank groups; the swizzle is
+// applied on the per-lane GLOBAL address, since an LDS-DMA writes lane l at base + 16 l.  One LDS
+// buffer (32 KiB) and two barriers per step: latency is hidden by 3-4 workgroups per CU.
+template <int EPI>
 __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
                                                     const float* __restrict__ bias, const uint16_t* __restrict__ R,
-                                                    uint16_t* __restrict__ C, int M, int N, int K, int epi) {
-    __shared__ __attribute__((aligned(16))) uint16_t sA[2][GB_M * LDS_ROW];
-    __shared__ __attribute__((aligned(16))) uint16_t sB[2][GB_N * LDS_ROW];
+                                                    uint16_t* __restrict__ C, int M, int N, int K) {
+    __shared__ __attribute__((aligned(16))) uint16_t smem[(GB_M + GB_N) * GB_K];
+    uint16_t* sA = smem;
+    uint16_t* sB = smem + GB_M * GB_K;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round robin (id % 8), so renumber them
-    // such that each XCD gets a contiguous run of tiles -- the N tiles of the same M row-block -- and
-    // the A rows they share stay in that XCD's L2
+    // XCD-aware tile order (bijective): workgroups are dealt to the 8 XCDs round robin, so give each
+    // XCD a contiguous run of tile ids -- the N tiles of one M row-block share their A rows in its L2
     const int tiles_n = N / GB_N;
-    const int nb = (int)gridDim.x;
-    const int bid = nb % 8 == 0 ? (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    const int nwg = (int)gridDim.x, orig = (int)blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
     const int tm = bid / tiles_n, tn = bid % tiles_n;
     const int m0 = tm * GB_M, n0 = tn * GB_N;
     const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-    // global -> register staging: each thread moves 2 16-byte chunks of A and 2 of W per K slab
-    // (128 rows x 64 B = 512 chunks per operand); chunk q: row q >> 2, 16-byte column q & 3
-    uint4 ra[2], rb[2];
-    auto gload = [&](int k0) {
+    // this lane's source rows / swizzled chunks for its 4 DMA instructions per operand
+    const uint16_t* srcA[4];
+    const uint16_t* srcB[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = tid + i * G_THREADS, row = q >> 2, col = (q & 3) * 8;
-            ra[i] = *reinterpret_cast<const uint4*>(A + (size_t)(m0 + row) * K + k0 + col);
-            rb[i] = *reinterpret_cast<const uint4*>(W + (size_t)(n0 + row) * K + k0 + col);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = tid + i * G_THREADS, row = q >> 2, col = (q & 3) * 8;
-            *reinterpret_cast<uint4*>(&sA[buf][row * LDS_ROW + col]) = ra[i];
-            *reinterpret_cast<uint4*>(&sB[buf][row * LDS_ROW + col]) = rb[i];
-        }
-    };
+    for (int i = 0; i < 4; ++i) {
+        const int q = (i * 4 + wave) * 64 + lane, row = q >> 3, pos = q & 7;
+        const int col = 8 * (pos ^ (row & 7));
+        srcA[i] = A + (size_t)(m0 + row) * K + col;
+        srcB[i] = W + (size_t)(n0 + row) * K + col;
+    }
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
     const int r = lane & 31, h = lane >> 5;
-    const int nk = K / GB_K;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) gload((kt + 1) * GB_K);          // next slab in flight during the MFMAs
+    for (int k0 = 0; k0 < K; k0 += GB_K) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int blk = (i * 4 + wave) * 64 * 8;      // this wave-instruction's 1 KiB of LDS
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcA[i] + k0), (lptr_t)(sA + blk), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcB[i] + k0), (lptr_t)(sB + blk), 16, 0, 0);
+        }
+        __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < GB_K / 16; ++ks) {
             bf16x8 fa[2], fb[2];
+            const int c = 2 * ks + h;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                fa[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm + 32 * i + r) * LDS_ROW + ks * 16 + 8 * h]);
-                fb[i] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn + 32 * i + r) * LDS_ROW + ks * 16 + 8 * h]);
+                const int ra = wm + 32 * i + r, rb = wn + 32 * i + r;
+                fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
+                fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -100,25 +104,61 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) lstore(buf ^ 1);
         __syncthreads();
     }
-    // epilogue: C/D map of 32x32x16: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+    // epilogue through LDS (the K loop left it free: 32 KiB), 64 rows at a time: the two wavefronts
+    // holding those rows store their accumulators as a row-major f32 [64][128] image (C/D map of
+    // 32x32x16: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)); then every thread
+    // finishes 8-column chunks with 16-byte loads of the residual and 16-byte stores of C
+    float* sC = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int half = 0; half < 2; ++half) {
+        if ((wave >> 1) == half) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn + 32 * j + r;
-            const float b = bias ? bias[col] : 0.f;
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = m0 + wm + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                float v = acc[i][j][reg] + b;
-                if (epi == EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-                else if (epi == EPI_RESID) v += bf2f(R[(size_t)row * N + col]);
-                C[(size_t)row * N + col] = f2bf(v);
-            }
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const int row = 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                        sC[row * GB_N + wn + 32 * j + r] = acc[i][j][reg];
+                    }
         }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int q = tid + t * G_THREADS, row = q >> 4, c8 = (q & 15) * 8;
+            const float4 x0 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8);
+            const float4 x1 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8 + 4);
+            float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            const int grow = m0 + 64 * half + row, gcol = n0 + c8;
+            if (bias) {
+                const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+                const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+                v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+                v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+            }
+            if (EPI == EPI_GELU) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+            } else if (EPI == EPI_RESID) {
+                const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)grow * N + gcol);
+                const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] += bf2f((uint16_t)(rw[e] & 0xffffu));
+                    v[2 * e + 1] += bf2f((uint16_t)(rw[e] >> 16));
+                }
+            }
+            uint4 o;
+            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+            o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = o;
+        }
+        __syncthreads();
+    }
     (void)M;
 }
 
@@ -241,6 +281,116 @@ __global__ __launch_bounds__(256) void k_attention(const uint16_t* __restrict__ 
     }
 }
 
+// Attention on the matrix cores, one workgroup (4 wavefronts) per (sequence, head), S <= 128 keys,
+// S % 32 == 0.  Wavefront w owns queries [32w, 32w + 32).
+//   X = K . Q^T  (32x32x16: A = K rows, B[d][query] = Q rows -- both K-contiguous)  -> X[key][query]:
+//   per lane one query (its column), the keys in its 16 registers x 4 key tiles x the 2 lane halves,
+//   so the softmax over keys is in-lane plus one shuffle across the halves.
+//   Y = V^T . P  sums over X's ROW index, so P (= exp(X - max), bf16) is the B operand straight from
+//   the accumulator registers (no lane movement); its k order inside a 16-step is permuted -- element
+//   j of lane half h is key 16s + 8(j >> 2) + 4h + (j & 3) -- and the A operand (V^T, staged
+//   transposed in LDS) is read in that same order.   O[query][d] = Y[d][query] / l[query].
+constexpr int AT_ROW = ATT_D + 8;          // Q / K LDS rows: 64 bf16 + 16 B pad
+constexpr int AT_VROW = 128 + 8;           // V^T LDS rows: 128 keys + 16 B pad
+__global__ __launch_bounds__(256) void k_attention_mfma(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask,
+                                                        uint16_t* __restrict__ out, int S, int heads) {
+    __shared__ __attribute__((aligned(16))) uint16_t sQ[128 * AT_ROW];
+    __shared__ __attribute__((aligned(16))) uint16_t sK[128 * AT_ROW];
+    __shared__ __attribute__((aligned(16))) uint16_t sVt[ATT_D * AT_VROW];
+    __shared__ int sM[128];
+    const int b = blockIdx.x / heads, hd = blockIdx.x % heads;
+    const int H = heads * ATT_D, W3 = 3 * H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // stage Q, K (row-major) and V^T; 16-byte chunks: row j = q >> 3, d = 8 (q & 7)
+    for (int q = tid; q < S * 8; q += 256) {
+        const int j = q >> 3, d = 8 * (q & 7);
+        const uint16_t* src = qkv + (size_t)(b * S + j) * W3 + hd * ATT_D + d;
+        *reinterpret_cast<uint4*>(sQ + j * AT_ROW + d) = *reinterpret_cast<const uint4*>(src);
+        *reinterpret_cast<uint4*>(sK + j * AT_ROW + d) = *reinterpret_cast<const uint4*>(src + H);
+        const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * H);
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sVt[(d + 2 * e) * AT_VROW + j] = (uint16_t)(vw[e] & 0xffffu);
+            sVt[(d + 2 * e + 1) * AT_VROW + j] = (uint16_t)(vw[e] >> 16);
+        }
+    }
+    for (int j = tid; j < 128; j += 256) sM[j] = (j < S) ? (mask ? mask[b * S + j] : 1) : 0;
+    __syncthreads();
+    const int q0 = 32 * wave;
+    if (q0 >= S) return;
+    const int r = lane & 31, h = lane >> 5;
+    const int nkt = S / 32;
+    f32x16 X[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) X[i] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < ATT_D / 16; ++ks) {
+        const bf16x8 fq = *reinterpret_cast<const bf16x8*>(sQ + (q0 + r) * AT_ROW + 16 * ks + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < nkt) {
+                const bf16x8 fk = *reinterpret_cast<const bf16x8*>(sK + (32 * i + r) * AT_ROW + 16 * ks + 8 * h);
+                X[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk, fq, X[i], 0, 0, 0);
+            }
+    }
+    // softmax over keys for this lane's query (key of register g in tile i: 32i + (g&3) + 8(g>>2) + 4h)
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int key = 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+            const float v = (i < nkt && sM[key]) ? X[i][g] * 0.125f : -3.0e38f;
+            X[i][g] = v;
+            mx = fmaxf(mx, v);
+        }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const float p = X[i][g] > -1.0e38f ? __expf(X[i][g] - mx) : 0.f;
+            X[i][g] = p;
+            l += p;
+        }
+    l += __shfl_xor(l, 32);
+    // Y[d][query] = sum_key V^T[d][key] P[key][query]
+    f32x16 Y[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < nkt) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                bf16x8 fp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fp[j] = (__bf16)X[i][8 * s2 + j];
+                const int kb = 32 * i + 16 * s2 + 4 * h;          // keys kb + {0..3} and kb + 8 + {0..3}
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const uint16_t* vr = sVt + (32 * t + r) * AT_VROW + kb;
+                    const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+                    const uint2 hi = *reinterpret_cast<const uint2*>(vr + 8);
+                    bf16x8 fv;
+                    const uint32_t w4[4] = {lo.x, lo.y, hi.x, hi.y};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        fv[2 * e] = __builtin_bit_cast(__bf16, (uint16_t)(w4[e] & 0xffffu));
+                        fv[2 * e + 1] = __builtin_bit_cast(__bf16, (uint16_t)(w4[e] >> 16));
+                    }
+                    Y[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fv, fp, Y[t], 0, 0, 0);
+                }
+            }
+        }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const size_t ob = (size_t)(b * S + q0 + r) * H + hd * ATT_D;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) out[ob + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * h] = f2bf(Y[t][g] * inv);
+}
+
 // logits[m][c] = h[m] . Wc[c] + bc[c]   (one wavefront per row)
 __global__ __launch_bounds__(256) void k_classify(const uint16_t* __restrict__ h, const uint16_t* __restrict__ Wc,
                                                   const float* __restrict__ bc, float* __restrict__ logits, int M,
@@ -264,9 +414,10 @@ int ner_gemm(const void* A, const void* W, const void* bias, const void* resid, 
     if (!A || !W || !C || M % GB_M || N % GB_N || K % GB_K || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !resid))
         return -1;
     const int blocks = (M / GB_M) * (N / GB_N);
-    k_gemm<<<blocks, G_THREADS, 0, static_cast<hipStream_t>(stream)>>>(
+    auto kern = epi == EPI_GELU ? k_gemm<EPI_GELU> : epi == EPI_RESID ? k_gemm<EPI_RESID> : k_gemm<EPI_BIAS>;
+    kern<<<blocks, G_THREADS, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(W), static_cast<const float*>(bias),
-        static_cast<const uint16_t*>(resid), static_cast<uint16_t*>(C), M, N, K, epi);
+        static_cast<const uint16_t*>(resid), static_cast<uint16_t*>(C), M, N, K);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -289,6 +440,11 @@ int ner_embed(const int32_t* ids, const void* wemb, const void* pemb, const void
 
 int ner_attention(const void* qkv, const int32_t* mask, void* out, int B, int S, int heads, int dhead, void* stream) {
     if (!qkv || !out || dhead != ATT_D || S <= 0 || S > ATT_SMAX || B <= 0 || heads <= 0) return -1;
+    if (S <= 128 && S % 32 == 0) {          // matrix-core path
+        k_attention_mfma<<<B * heads, 256, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const uint16_t*>(qkv), mask, static_cast<uint16_t*>(out), S, heads);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     const size_t lds = (size_t)S * ATT_D * 2 * sizeof(float) + (size_t)S * sizeof(int);
     static bool raised = false;
     if (lds > 64 * 1024 && !raised) {

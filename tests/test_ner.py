@@ -39,7 +39,7 @@ def _bf(x):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (256, 384, 96), (1024, 2304, 768), (512, 768, 3072)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (1024, 2304, 768), (512, 768, 3072)])
 def test_gemm_vs_torch(ner_model, M, N, K):
     import torch
     Nm = pkg("ner")
@@ -73,19 +73,21 @@ def test_layernorm_and_attention_vs_torch(ner_model):
     m.layernorm(x.to(dev, torch.bfloat16), gam.to(dev), bet.to(dev), out)
     want = torch.nn.functional.layer_norm(_bf(x), (768,), gam, bet, eps=m.eps)
     assert (out.float().cpu() - want).abs().max().item() < 0.05
-    # attention over the fused QKV rows, with padded keys masked
-    B, S, Hh = 2, 64, 12
-    qkv = torch.randn(B * S, 3 * 768, generator=g)
-    mask = torch.ones(B, S, dtype=torch.int32)
-    mask[1, 40:] = 0
-    ctx = torch.zeros(B * S, 768, dtype=torch.bfloat16, device=dev)
-    rc = m.lib.ner_attention(qkv.to(dev, torch.bfloat16).data_ptr(), mask.to(dev).data_ptr(), ctx.data_ptr(), B, S,
-                             Hh, 64, m._st())
-    assert rc == 0
-    q, k, v = (_bf(qkv).reshape(B, S, 3, Hh, 64)[:, :, i].transpose(1, 2) for i in range(3))
-    sc = q @ k.transpose(-1, -2) / 8.0 + (1 - mask[:, None, None, :].float()) * -1e30
-    want = (sc.softmax(-1) @ v).transpose(1, 2).reshape(B * S, 768)
-    assert (ctx.float().cpu() - want).abs().max().item() < 0.03
+    # attention over the fused QKV rows, with padded keys masked: the matrix-core kernel (S % 32 == 0,
+    # S <= 128) and the general one
+    for B, S in ((2, 64), (3, 128), (2, 48), (1, 160)):
+        Hh = 12
+        qkv = torch.randn(B * S, 3 * 768, generator=g)
+        mask = torch.ones(B, S, dtype=torch.int32)
+        mask[-1, S * 5 // 8:] = 0
+        ctx = torch.zeros(B * S, 768, dtype=torch.bfloat16, device=dev)
+        rc = m.lib.ner_attention(qkv.to(dev, torch.bfloat16).data_ptr(), mask.to(dev).data_ptr(), ctx.data_ptr(), B, S,
+                                 Hh, 64, m._st())
+        assert rc == 0
+        q, k, v = (_bf(qkv).reshape(B, S, 3, Hh, 64)[:, :, i].transpose(1, 2) for i in range(3))
+        sc = q @ k.transpose(-1, -2) / 8.0 + (1 - mask[:, None, None, :].float()) * -1e30
+        want = (sc.softmax(-1) @ v).transpose(1, 2).reshape(B * S, 768)
+        assert (ctx.float().cpu() - want).abs().max().item() < 0.03, S
 
 
 @pytest.mark.gpu
