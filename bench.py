@@ -171,6 +171,7 @@ class DeviceBatch:
         self.slot = torch.from_numpy((self.meta.conv_slot - conv_base).view(np.int32)).to(dev)
         self.role = torch.from_numpy(self.meta.role).to(dev)
         self.ts = torch.from_numpy(self.meta.ts_us).to(dev)
+        n_utt = self.n                     # capacities follow the utterance count, also for long rows
         if join > 1:
             # long rows (whole transcripts, ccai_insights_function/main.py:47-50): every `join`
             # consecutive utterances form one row, redacted without role context (ROLE_OTHER)
@@ -180,8 +181,8 @@ class DeviceBatch:
             self.slot = torch.arange(self.n, dtype=torch.int32, device=dev) % max(C, 1)
             self.role = torch.full((self.n,), 2, dtype=torch.uint8, device=dev)
             self.ts = self.ts[:self.n].contiguous()
-        self.out_cap = self.n_bytes + 48 * self.n
-        self.span_cap = self.n * 2
+        self.out_cap = self.n_bytes + 48 * n_utt
+        self.span_cap = n_utt * 2
         self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
         self.out_offs = torch.empty(self.n + 1, dtype=torch.int64, device=dev)
         self.spans = torch.empty(self.span_cap * 16, dtype=torch.uint8, device=dev)
