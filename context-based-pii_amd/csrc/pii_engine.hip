@@ -321,6 +321,7 @@ __global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __res
 // table entries are absolute LDS byte addresses of the next row, bit 0 = accept (scan_tables); k_scan
 // has no static LDS, so its dynamic region starts at LDS address 0 and an entry IS the address
 constexpr uint32_t SCAN_TD_BASE = 1024;     // after the 256-entry class map
+constexpr uint32_t SCAN_SPREAD_BYTES = 512; // k_scan's 256 group masks (scan_spread), after the K table
 typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
 __device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
     return *reinterpret_cast<lds_u16_t*>((size_t)addr);
@@ -335,11 +336,10 @@ __device__ __forceinline__ uint32_t scan_state(uint32_t nd, uint32_t nk) { retur
 __device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* __restrict__ text, const Lane& L) {
     const uint32_t top = (uint32_t)min<int64_t>((int64_t)L.hi + SCAN_HALO, g_off(g, L.u1));
     const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)(R.SD * R.CDs / 2) * 4;
-    const uint32_t start2 = (uint32_t)R.d_start | ((uint32_t)R.k_start << 16);
     const uint8_t* tb = text + g.base;
     uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
     for (int64_t b = (int64_t)top - 1; b >= (int64_t)L.hi; --b) {
-        const uint32_t x = R.cmap4[tb[b]] + (pm & start2);
+        const uint32_t x = R.cmap4[tb[b]];
         const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
         const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
         nd = R.td[(ad - SCAN_TD_BASE) >> 1];
@@ -405,16 +405,46 @@ __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t ab, u
     }
 }
 
+// the group mask for utterance-start bits sb (bit j: byte j starts one): every accept bit (even bits),
+// and the end-of-text bit 2 (7 - j) + 1 of each starting byte j (the m layout of SCAN_STEP8)
+__device__ __forceinline__ uint32_t scan_spread(uint32_t sb) {
+    uint32_t v = 0x5555u;
+    for (int j = 0; j < 8; ++j)
+        if (sb >> j & 1u) v |= 1u << (2 * (7 - j) + 1);
+    return v;
+}
+
+// class word of byte K of a 16-byte chunk: the class map sits at LDS address 0, so the address is
+// byte * 4 -- one SDWA shift of the byte lane of its dword
+template <int K>
+__device__ __forceinline__ uint32_t class_of(const uint4& w) {
+    const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
+    uint32_t a;
+    if constexpr ((K & 3) == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+            : "=v"(a) : "v"(x));
+    else if constexpr ((K & 3) == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+            : "=v"(a) : "v"(x));
+    else if constexpr ((K & 3) == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(a) : "v"(x));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+            : "=v"(a) : "v"(x));
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)a);
+}
+
 // byte classes of 8 bytes (HALF = 0: bytes 8..15 of the chunk, 1: bytes 0..7), issued together
 #define SCAN_CLASSES8(W, H)                                                                       \
-    cc[0] = s_cmap[byte_c<(H) + 0>(W)];                                                           \
-    cc[1] = s_cmap[byte_c<(H) + 1>(W)];                                                           \
-    cc[2] = s_cmap[byte_c<(H) + 2>(W)];                                                           \
-    cc[3] = s_cmap[byte_c<(H) + 3>(W)];                                                           \
-    cc[4] = s_cmap[byte_c<(H) + 4>(W)];                                                           \
-    cc[5] = s_cmap[byte_c<(H) + 5>(W)];                                                           \
-    cc[6] = s_cmap[byte_c<(H) + 6>(W)];                                                           \
-    cc[7] = s_cmap[byte_c<(H) + 7>(W)];
+    cc[0] = class_of<(H) + 0>(W);                                                                 \
+    cc[1] = class_of<(H) + 1>(W);                                                                 \
+    cc[2] = class_of<(H) + 2>(W);                                                                 \
+    cc[3] = class_of<(H) + 3>(W);                                                                 \
+    cc[4] = class_of<(H) + 4>(W);                                                                 \
+    cc[5] = class_of<(H) + 5>(W);                                                                 \
+    cc[6] = class_of<(H) + 6>(W);                                                                 \
+    cc[7] = class_of<(H) + 7>(W);
 
 // v[j] for a per-lane j in 0..7 (a select tree: the arrays stay in registers)
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t j) {
@@ -449,28 +479,32 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, 
     } while (m);
 }
 
-// One byte of both reverse automata.  nd/nk are the raw entries of the previous step; pm is all ones
-// iff the previous byte started an utterance, and then the row becomes the start row without a
-// branch: (entry & ~pm & ~3) + (class + (pm & start)).  Rows and classes stay below 64 KiB, so the
-// packed class pair + packed start pair add without a carry between the halves.  The two dependent
-// ALU ops between LDS reads are the whole per-byte chain; flags go to m and are emitted per 8 bytes.
+// One byte of both reverse automata.  nd/nk are the raw entries of the previous step: the destination
+// row's offset from the START row (relayout puts the start state first) | flags.  pm is all ones iff
+// the previous byte started an utterance, and then the row becomes the start row without a branch:
+// (entry & ~pm & ~3) + class, the class word carrying the table bases (both halves stay below 64 KiB,
+// so nothing carries between them).  The two dependent ALU ops between LDS reads are the whole
+// per-byte chain.  Both flag bits of every byte are shifted into the top of m (one alignbit: byte j
+// ends at bits 16 + 2 (7 - j)); the group's spread mask (LDS, indexed by its utterance-start bits)
+// then keeps an end-of-text accept only on a byte that starts an utterance.
 #define SCAN_STEP8(J, H)                                                                          \
     {                                                                                             \
-        const uint32_t x = cc[J] + (pm & start2);                                                 \
-        ad[J] = (nd & ~pm & 0xfffcu) + (x & 0xffffu);                                             \
-        ak[J] = (nk & ~pm & 0xfffcu) + (x >> 16);                                                 \
+        ad[J] = (nd & ~pm & 0xfffcu) + (cc[J] & 0xffffu);                                         \
+        ak[J] = (nk & ~pm & 0xfffcu) + (cc[J] >> 16);                                             \
         nd = lds_u16(ad[J]);                                                                      \
         nk = lds_u16(ak[J]);                                                                      \
-        pm = (uint32_t)((int32_t)(b16 << (31 - (H) - (J))) >> 31);                                \
-        m |= ((nd | nk) & ((pm & 2u) | 1u)) << (2 * (7 - (J)));                                   \
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(pm) : "v"(b16), "n"((H) + (J)));                   \
+        m = __builtin_amdgcn_alignbit(nd | nk, m, 2);                                             \
     }
 
 #define SCAN_GROUP8(W, H, OFF)                                                                    \
     {                                                                                             \
         uint32_t cc[8], ad[8], ak[8], m = 0;                                                      \
         SCAN_CLASSES8(W, H)                                                                       \
+        const uint32_t mk = lds_u16(spread + 2u * ((b16 >> (H)) & 0xffu));                        \
         SCAN_STEP8(7, H) SCAN_STEP8(6, H) SCAN_STEP8(5, H) SCAN_STEP8(4, H)                       \
         SCAN_STEP8(3, H) SCAN_STEP8(2, H) SCAN_STEP8(1, H) SCAN_STEP8(0, H)                       \
+        m = (m >> 16) & mk;                                                                       \
         if (__builtin_expect(m != 0, 0))                                                          \
             scan_emit8(ev, ab, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
     }
@@ -499,7 +533,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
                                                      const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     if (*err & ERR_ARGS) return;              // the declared batch size was wrong: nothing is sized for it
-    uint32_t* s_cmap = smem32;                                   // 256 x (2*classD | 2*classK << 16)
+    // LDS: class map at 0 (256 x class words: D base + 2 classD | (K base + 2 classK) << 16), D table,
+    // K table, group masks
     const int nd_words = R.SD * R.CDs / 2;      // rows padded to an even class count
     const int nk_words = R.SK * R.CKs / 2;
     const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)nd_words * 4;
@@ -511,6 +546,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
         for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
         for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
         for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
+        uint32_t* d_sp = d_tk + nk_words;
+        for (int i = threadIdx.x; i < 128; i += blockDim.x) d_sp[i] = scan_spread(2 * i) | scan_spread(2 * i + 1) << 16;
     }
     __syncthreads();
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
@@ -526,9 +563,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
         uint32_t lo_r, len_r;
         emit_range(L, lo_r, len_r);
         const uint32_t ab = (uint32_t)ev_base(L, c);
-        const uint32_t d_start = (uint32_t)R.d_start, k_start = (uint32_t)R.k_start;
-        const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
-        const uint32_t start2 = d_start | (k_start << 16);
+        const uint32_t eot_d = SCAN_TD_BASE + 2u * (uint32_t)(R.CD - 1), eot_k = tk_base + 2u * (uint32_t)(R.CK - 1);
+        const uint32_t spread = tk_base + (uint32_t)nk_words * 4;     // scan_spread table (after K)
         // "previous byte started an utterance": start rows; a lane cut at hi continues from its halo state
         uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
         if (L.chi) {
@@ -591,8 +627,7 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
     const uint32_t ab = (uint32_t)ev_base(L, c);
     const uint32_t nd_words = (uint32_t)(R.SD * R.CDs / 2);
     const uint32_t tk_base = SCAN_TD_BASE + nd_words * 4;
-    const uint32_t eot_d = 2u * (uint32_t)(R.CD - 1), eot_k = 2u * (uint32_t)(R.CK - 1);
-    const uint32_t start2 = (uint32_t)R.d_start | ((uint32_t)R.k_start << 16);
+    const uint32_t eot_d = SCAN_TD_BASE + 2u * (uint32_t)(R.CD - 1), eot_k = tk_base + 2u * (uint32_t)(R.CK - 1);
     const uint8_t* tb = text + g.base;
     uint32_t nd = entry & 0xffffu, nk = entry >> 16, pm = 0;
     uint32_t cnt = 0;
@@ -603,7 +638,7 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
         --v;
     for (int64_t b = (int64_t)L.hi - 1; b >= (int64_t)L.lo; --b) {
         const uint32_t cls = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)(4u * tb[b]));
-        const uint32_t x = cls + (pm & start2);
+        const uint32_t x = cls;
         const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
         const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
         nd = lds_u16(ad);
@@ -3813,30 +3848,34 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     // entry (row, class) = address of the destination row | accept | accept of the destination's
     // end-of-text transition (class C-1) << 1, so k_scan resets at an utterance start without
     // reading the end-of-text entry
-    auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, uint32_t base,
-                       uint16_t* t, uint16_t* a) {
+    // (k_scan: rows are placed with the START state first -- row = pos(state) -- and entries are the
+    // destination row's byte offset from the table base, so a reset is "row 0"; the class words carry
+    // the table bases; accept-id tables follow the same placement)
+    auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, int start, uint16_t* t,
+                       uint16_t* a) {
+        auto pos = [start](uint32_t r) { return r == (uint32_t)start ? 0u : r == 0 ? (uint32_t)start : r; };
         for (int r = 0; r < S; ++r)
             for (int c = 0; c < C; ++c) {
                 const uint32_t v = s[r * C + c], dst = v & 0x7fff;
                 const uint32_t eot = s[dst * C + C - 1] >> 15;
-                t[r * Cs + c] = (uint16_t)((base + dst * Cs * 2) | (v >> 15) | (eot << 1));
-                a[r * Cs + c] = acc[r * C + c];
+                t[pos(r) * Cs + c] = (uint16_t)((pos(dst) * Cs * 2) | (v >> 15) | (eot << 1));
+                a[pos(r) * Cs + c] = acc[r * C + c];
             }
     };
     {
         relayout(reinterpret_cast<const uint16_t*>(find("scan.d.trans")->data),
-                 reinterpret_cast<const uint16_t*>(find("scan.d.accid")->data), R.SD, R.CD, R.CDs, SCAN_TD_BASE,
+                 reinterpret_cast<const uint16_t*>(find("scan.d.accid")->data), R.SD, R.CD, R.CDs, R.d_start,
                  td.data(), dacc.data());
         relayout(reinterpret_cast<const uint16_t*>(find("scan.k.trans")->data),
-                 reinterpret_cast<const uint16_t*>(find("scan.k.accid")->data), R.SK, R.CK, R.CKs, tk_base,
+                 reinterpret_cast<const uint16_t*>(find("scan.k.accid")->data), R.SK, R.CK, R.CKs, R.k_start,
                  tk.data(), kacc.data());
     }
-    R.d_start = (int)(SCAN_TD_BASE + R.d_start * R.CDs * 2);     // start rows as LDS byte addresses
-    R.k_start = (int)(tk_base + R.k_start * R.CKs * 2);
+    R.d_start = R.k_start = 0;                                     // row offsets: the start rows are first
     std::vector<uint32_t> cmap4(256);
     {
         const uint16_t* c2 = reinterpret_cast<const uint16_t*>(find("scan.cmap2")->data);
-        for (int b = 0; b < 256; ++b) cmap4[b] = 2u * (c2[b] & 0xffu) | (2u * (uint32_t)(c2[b] >> 8)) << 16;
+        for (int b = 0; b < 256; ++b)
+            cmap4[b] = (SCAN_TD_BASE + 2u * (c2[b] & 0xffu)) | (tk_base + 2u * (uint32_t)(c2[b] >> 8)) << 16;
     }
     std::vector<uint16_t> k_acc_min;
     {
@@ -3903,17 +3942,18 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             if (!sc || !st || !sa || st->bytes != (size_t)h.SD * h.CD * 2 || sa->bytes != st->bytes || sc->bytes != 256)
                 return fail("SCAN group tables malformed");
             const uint32_t tkb = SCAN_TD_BASE + (uint32_t)(h.SD * h.CDs) * 2;
-            h.lds = tkb + 4;                                    // + the K stub's row (2 entries)
+            h.lds = tkb + 4 + SCAN_SPREAD_BYTES;                // + the K stub's row (2 entries), spread masks
             if (h.lds > 65536) return fail("a SCAN group exceeds 64 KiB of LDS");
             h.td.assign((size_t)h.SD * h.CDs, 0);
             h.dacc.assign((size_t)h.SD * h.CDs, 0);
+            if (gm[2] < 0 || gm[2] >= h.SD) return fail("SCAN group start state out of range");
             relayout(reinterpret_cast<const uint16_t*>(st->data), reinterpret_cast<const uint16_t*>(sa->data), h.SD,
-                     h.CD, h.CDs, SCAN_TD_BASE, h.td.data(), h.dacc.data());
-            h.tk = {(uint16_t)tkb, (uint16_t)tkb};
+                     h.CD, h.CDs, (int)gm[2], h.td.data(), h.dacc.data());
+            h.tk = {0, 0};
             h.kacc = {0, 0};
-            h.start = (int)(SCAN_TD_BASE + gm[2] * h.CDs * 2);
+            h.start = 0;
             h.cmap4.resize(256);
-            for (int b = 0; b < 256; ++b) h.cmap4[b] = 2u * sc->data[b];        // K stub: class 0
+            for (int b = 0; b < 256; ++b) h.cmap4[b] = (SCAN_TD_BASE + 2u * sc->data[b]) | tkb << 16;   // K stub: class 0
             hg.push_back(std::move(h));
         }
     }
@@ -4058,7 +4098,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
-    e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4;
+    e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4 + SCAN_SPREAD_BYTES;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     e->n_sg = 1 + (uint32_t)hg.size();
     e->sg.assign(1, R);
@@ -4079,7 +4119,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         Rq.SK = 1;
         Rq.CK = 2;
         Rq.CKs = 2;
-        Rq.k_start = (int)(h.lds - 4);
+        Rq.k_start = 0;
         e->sg.push_back(Rq);
         e->sg_lds.push_back(h.lds);
         e->acct.accid[q + 1] = Rq.d_accid;
