@@ -75,6 +75,8 @@ struct RulesDev {
     const uint16_t* d_acc_ids;
     const uint16_t* k_accid;  // [SK*CKs]
     const uint16_t* k_acc_min;  // per K accept set: smallest context group
+    const uint16_t* d_npair;    // [SD*CDs] per D transition: pairs of its accept set (k_pairs count pass)
+    const uint16_t* k_grp;      // [SK*CKs] per K transition: smallest context group it accepts, or KW_NONE
     const uint16_t* det_type;
     const uint8_t* det_val;
     const uint8_t* det_lik;
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo
     {
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
         const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
-        uint32_t* d_td = smem32 + 256;
+        uint32_t* d_td = smem32 + SCAN_TD_BASE / 4;
         uint32_t* d_tk = d_td + nd_words;
         for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
         for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
@@ -682,7 +684,7 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g,
         const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
         const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
-        uint32_t* d_td = smem32 + 256;
+        uint32_t* d_td = smem32 + SCAN_TD_BASE / 4;
         uint32_t* d_tk = d_td + nd_words;
         for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
         for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
@@ -1083,9 +1085,14 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
         int grp = KW_NONE;
         for (uint32_t k = 0; k < cnt; ++k) {
             Event E;
-            uint32_t acc;
-            bool k0;
-            next(E, acc, k0);
+            uint32_t acc = 0;
+            bool k0 = true;
+            if (MULTI) {
+                next(E, acc, k0);
+            } else {                        // one list: per-transition pair counts / keyword groups
+                E = En;
+                if (k + 1 < cnt) En = evl[k + 1];
+            }
             const int64_t pos = E.pos;
             while (pos < s_u) {
                 if (grp != KW_NONE) put_kw(u, grp);
@@ -1094,10 +1101,15 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
                 s_u = uoff(u);
                 agent = uagent(u);
             }
-            np += acc_off(acc + 1) - acc_off(acc);
-            if (agent && k0) {
-                const uint32_t a = R.k_accid[E.sk];
-                if (a) grp = min(grp, (int)kmin(a));
+            if (MULTI) {
+                np += acc_off(acc + 1) - acc_off(acc);
+                if (agent && k0) {
+                    const uint32_t a = R.k_accid[E.sk];
+                    if (a) grp = min(grp, (int)kmin(a));
+                }
+            } else {
+                np += R.d_npair[E.sd];
+                if (agent) grp = min(grp, (int)R.k_grp[E.sk]);
             }
         }
         if (cnt && grp != KW_NONE) put_kw(u, grp);
@@ -3975,6 +3987,13 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     size_t i_cmap = add(cmap4.data(), cmap4.size() * 4), i_td = add(td.data(), td.size() * 2), i_tk = add(tk.data(), tk.size() * 2);
     size_t i_dacc = add(dacc.data(), dacc.size() * 2), i_doff = addsec("scan.d.acc_off"), i_dids = addsec("scan.d.acc_ids");
     size_t i_kacc = add(kacc.data(), kacc.size() * 2), i_kmin = add(k_acc_min.data(), k_acc_min.size() * 2);
+    std::vector<uint16_t> d_npair(dacc.size()), k_grp(kacc.size());
+    {
+        const uint32_t* off = reinterpret_cast<const uint32_t*>(find("scan.d.acc_off")->data);
+        for (size_t i = 0; i < dacc.size(); ++i) d_npair[i] = (uint16_t)(off[dacc[i] + 1] - off[dacc[i]]);
+        for (size_t i = 0; i < kacc.size(); ++i) k_grp[i] = kacc[i] ? k_acc_min[kacc[i]] : (uint16_t)KW_NONE;
+    }
+    size_t i_dnp = add(d_npair.data(), d_npair.size() * 2), i_kgrp = add(k_grp.data(), k_grp.size() * 2);
     size_t i_dt = addsec("det.type"), i_dv = addsec("det.validator"), i_dl = addsec("det.lik"),
            i_dx = addsec("det.exidx"), i_fd = addsec("det.first_desc"), i_hr = addsec("hot.rule"),
            i_hd = addsec("hot.dfa_desc"), i_ve = addsec("var.enabled"), i_vm = addsec("var.minlik"),
@@ -4001,6 +4020,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     R.d_acc_ids = (const uint16_t*)at(i_dids);
     R.k_accid = (const uint16_t*)at(i_kacc);
     R.k_acc_min = (const uint16_t*)at(i_kmin);
+    R.d_npair = (const uint16_t*)at(i_dnp);
+    R.k_grp = (const uint16_t*)at(i_kgrp);
     R.det_type = (const uint16_t*)at(i_dt);
     R.det_val = (const uint8_t*)at(i_dv);
     R.det_lik = (const uint8_t*)at(i_dl);
@@ -4098,7 +4119,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
-    e->scan_lds = 1024 + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4 + SCAN_SPREAD_BYTES;
+    e->scan_lds = SCAN_TD_BASE + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4 + SCAN_SPREAD_BYTES;
     if (e->scan_lds > 160 * 1024) return fail("SCAN tables do not fit in LDS");
     e->n_sg = 1 + (uint32_t)hg.size();
     e->sg.assign(1, R);
