@@ -1161,6 +1161,138 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     }
 }
 
+// One SCAN group: the same two passes, wave-cooperative.  A wavefront's 64 lanes own consecutive
+// blocks of the event numbering (lane_ev), so their events are processed as one flattened list, 64
+// at a time: event f belongs to the first lane whose inclusive event count exceeds f (a 6-step
+// shuffle search), its utterance is found by a binary search over that lane's staged utterance
+// offsets, and every per-event record is written at E0 + f -- 64 neighbouring records per store
+// instead of record k of 64 lanes (the per-lane walk is a serial chain of dependent loads, and its
+// stores land in 64 different lines).  Pair numbering per lane is back to front (ascending by start,
+// as the per-lane form): a segmented scan of the events' pair counts plus each lane's running total.
+// Keyword groups of AGENT rows are merged with atomic min (init: k_chunk_index).
+template <bool WRITE>
+__global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, const Geo g,
+                                                    const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
+                                                    const uint8_t* __restrict__ role, int32_t* __restrict__ kw,
+                                                    EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
+                                                    uint64_t pair_cap, uint64_t ev_cap,
+                                                    const uint64_t* __restrict__ lane_pair,
+                                                    const uint64_t* __restrict__ lane_ev,
+                                                    uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
+    __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
+    if (*err & ERR_ARGS) return;
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t n_chunks = g.n_chunks;
+    const uint64_t* __restrict__ offs = g.offs;
+    const int64_t base = (int64_t)g.base;
+    const uint32_t cw0 = c - lane;
+    const uint32_t cw1 = min(cw0 + 64, n_chunks);
+    const uint32_t U0 = cw0 < n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
+    const uint32_t U1 = cw0 < n_chunks ? g.first_utt[cw1] : 0u;
+    const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
+    uint32_t* so = s_off[wv];
+    uint8_t* sr = s_role[wv];
+    if (staged && cw0 < n_chunks) {
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)((int64_t)offs[U0 + k] - base);
+        if (!WRITE)
+            for (uint32_t k = lane; k < U1 - U0; k += 64) sr[k] = role[U0 + k];
+    }
+    __syncthreads();
+    if (cw0 >= n_chunks) return;
+    auto uoff = [&](uint32_t u) { return staged ? so[u - U0] : (uint32_t)((int64_t)offs[u] - base); };
+    const bool valid = c < n_chunks;
+    const uint32_t cnt = valid ? lane_cnt[c] : 0u;
+    uint32_t eb = 0, u0 = 0, u1 = 0;                      // the lane's arena, utterances [u0, u1)
+    if (cnt) {
+        const Lane L = g_lane(g, c);
+        eb = (uint32_t)ev_base(L, c);
+        u0 = L.u0;
+        u1 = L.u1;
+    }
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 63), excl = incl - cnt;
+    uint64_t E0 = 0, top = 0;            // WRITE: the wave's first event record; lane: its last pair + 1
+    if (WRITE) {
+        E0 = lane_ev[cw0];
+        top = valid ? lane_pair[c] + lane_np[c] : 0;
+        const bool over = (valid && top > pair_cap) || E0 + total > ev_cap;
+        if (__any(over)) {
+            if (lane == 0) atomicOr(err, (uint32_t)ERR_QUEUE);
+            return;
+        }
+    }
+    uint32_t run = 0;                                     // lane: pairs of its events handled so far
+    for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+        const uint32_t f = f0 + lane;
+        const bool act = f < total;
+        int ow = 0;                                       // owner: first lane with incl > f
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            const uint32_t v = __shfl(incl, ow + step - 1);
+            if (v <= f) ow += step;
+        }
+        const uint32_t o_ex = __shfl(excl, ow), o_eb = __shfl(eb, ow);
+        const uint32_t o_u0 = __shfl(u0, ow), o_u1 = __shfl(u1, ow), o_run = __shfl(run, ow);
+        const uint64_t o_top = WRITE ? __shfl(top, ow) : 0;
+        Event E{};
+        uint32_t n = 0, acc = 0, u = 0;
+        if (act) {
+            E = ev[(uint64_t)o_eb + (f - o_ex)];
+            n = R.d_npair[E.sd];
+            if (WRITE) acc = R.d_accid[E.sd];
+            uint32_t lo = o_u0, hi = o_u1 - 1;            // last u with start <= pos
+            while (lo < hi) {
+                const uint32_t m = (lo + hi + 1) >> 1;
+                if (uoff(m) <= E.pos) lo = m;
+                else hi = m - 1;
+            }
+            u = lo;
+        }
+        // pairs of the owner's events up to and including this one (segmented inclusive scan)
+        uint32_t sc = n;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(sc, d);
+            const int oo = __shfl_up(ow, d);
+            if (lane >= d && oo == ow) sc += o;
+        }
+        if (act) {
+            if (WRITE) {
+                EvPairs ep;
+                ep.first = (uint32_t)(o_top - (o_run + sc));
+                ep.acc = (uint16_t)acc;
+                ep.n = (uint16_t)n;
+                evpairs[E0 + f] = ep;
+                if (n) {
+                    EvLoc Lc;
+                    Lc.u = u;
+                    Lc.s = E.pos;
+                    Lc.ustart = uoff(u);
+                    Lc.uend = uoff(u + 1);
+                    evloc[E0 + f] = Lc;
+                }
+            } else {
+                const uint32_t kg = R.k_grp[E.sk];
+                if (kg != (uint32_t)KW_NONE && (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT)
+                    atomicMin(reinterpret_cast<unsigned int*>(kw + u), kg);
+            }
+        }
+        // each lane adds its events' pairs of this chunk (the scan value at its last slot here)
+        const bool here = cnt && incl > f0 && excl < f0 + 64;
+        const int last = here ? (int)(min(incl, f0 + 64) - 1 - f0) : 0;
+        const uint32_t add = __shfl(sc, last);
+        if (here) run += add;
+    }
+    if (!WRITE && valid) lane_np[c] = run;
+}
+
 // one thread per event: its (start, pattern) pairs, accept-set order (excluders first)
 __global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs* __restrict__ evpairs,
                                                 const uint64_t* __restrict__ ev_count, const uint32_t* __restrict__ err,
@@ -3547,10 +3679,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                                   e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
                                                                   e->lane_evn);
             else
-                k_pairs<false, false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                   e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                   e->lane_ev, e->lane_np, e->d_err, ns, es, cs,
-                                                                   e->acct, nullptr);
+                k_pairs_flat<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                 e->lane_ev, e->lane_np, e->d_err);
             int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
             if ((rc = exclusive_scan(e, multi ? e->lane_evn : e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
@@ -3560,10 +3691,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
                                                                  e->lane_evn);
             else
-                k_pairs<true, false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs,
-                                                                  e->acct, nullptr);
+                k_pairs_flat<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                e->lane_ev, e->lane_np, e->d_err);
             k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
         }
         HIPCHK(hipGetLastError());
