@@ -64,18 +64,31 @@ __device__ __forceinline__ void shr8(uint4& w) {
 }
 
 // Iterate the bytes of text[lo, hi) in order: BODY sees `c` (the byte) and `i` (its index relative
-// to lo).  One window load per 16 bytes, a runtime loop per byte (a wavefront leaves it as soon as
-// its last lane is done, instead of stepping through whole predicated chunks).
+// to lo).  The aligned 16-byte chunks holding the range are each loaded once, the next one issued
+// before the current one is stepped (the per-byte DFA chain hides its latency); a runtime loop per
+// byte (a wavefront leaves it as soon as its last lane is done, instead of stepping through whole
+// predicated chunks).
 #define PII_FOR_BYTES(text, lo, hi, ...)                                                         \
-    for (int _j = (lo); _j < (hi); _j += 16) {                                                    \
-        const int _n = (hi) - _j < 16 ? (hi) - _j : 16;                                           \
-        uint4 _w = load16((text) + _j, 0, _n);                                                    \
-        for (int _k = 0; _k < _n; ++_k) {                                                         \
-            const uint32_t c = _w.x & 0xffu;                                                      \
-            const int i = _j - (lo) + _k;                                                         \
-            (void)i;                                                                              \
-            __VA_ARGS__;                                                                          \
-            shr8(_w);                                                                             \
+    {                                                                                             \
+        const int _lo = (lo), _hi = (hi);                                                         \
+        if (_lo < _hi) {                                                                          \
+            const uintptr_t _s = (uintptr_t)((text) + _lo), _e = (uintptr_t)((text) + _hi);       \
+            uintptr_t _a = _s & ~(uintptr_t)15;                                                   \
+            uint32_t _skip = (uint32_t)(_s - _a);                                                 \
+            uint4 _nx = gload16(_a);                                                              \
+            int i = 0;                                                                            \
+            for (; _a < _e; _a += 16) {                                                           \
+                uint4 _w = _nx;                                                                   \
+                if (_a + 16 < _e) _nx = gload16(_a + 16);                                         \
+                if (_skip) _w = window16(_w, make_uint4(0, 0, 0, 0), _skip);                      \
+                const int _n = (int)((_e - _a < 16 ? _e - _a : 16) - _skip);                      \
+                _skip = 0;                                                                        \
+                for (int _k = 0; _k < _n; ++_k, ++i) {                                            \
+                    const uint32_t c = _w.x & 0xffu;                                              \
+                    __VA_ARGS__;                                                                  \
+                    shr8(_w);                                                                     \
+                }                                                                                 \
+            }                                                                                     \
         }                                                                                         \
     }
 

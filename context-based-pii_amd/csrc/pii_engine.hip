@@ -38,8 +38,8 @@ namespace {
 constexpr int P_MAX = 64;          // detector patterns handled by k_select's private state
 constexpr int NE_MAX = 2;          // excluder patterns
 constexpr int SCAN_BLOCK = 512;
-constexpr int CTX_BLOCK = 1024;
-constexpr int SCAN_ITEMS = 4;      // items per thread in the offset scans
+constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
+constexpr int SCAN_ITEMS = 8;      // items per thread in the offset scans (blocked, 16-byte accesses)
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
 #ifndef BYTES_PER_LANE_N
 #define BYTES_PER_LANE_N 1024
@@ -106,6 +106,7 @@ struct RulesDev {
 struct Geo {
     const uint64_t* offs;
     const uint32_t* first_utt;
+    const uint4* lanes;     // per lane {lo, hi, u0 | clo << 31, u1 | chi << 31} (k_lane_count); null before
     uint64_t base;          // offs[0]
     uint32_t n_utt, n_chunks, sh, r0, long_min;
 };
@@ -129,7 +130,7 @@ __device__ __forceinline__ bool g_cut(const Geo& g, uint32_t k) {
     return p > s && p < e && (e - s) > (int64_t)g.long_min;
 }
 
-__device__ __forceinline__ Lane g_lane(const Geo& g, uint32_t c) {
+__device__ __forceinline__ Lane g_lane_slow(const Geo& g, uint32_t c) {
     Lane L;
     const uint32_t f0 = g.first_utt[c], f1 = g.first_utt[c + 1];
     L.clo = g_cut(g, c);
@@ -138,6 +139,23 @@ __device__ __forceinline__ Lane g_lane(const Geo& g, uint32_t c) {
     L.hi = (uint32_t)(L.chi ? g_cpos(g, c + 1) : g_off(g, f1));
     L.u0 = L.clo ? f0 - 1 : f0;
     L.u1 = f1;
+    return L;
+}
+
+// (rows are < 2^31: the host bounds bytes + 2 * rows below 2^32)
+__device__ __forceinline__ uint4 lane_pack(const Lane& L) {
+    return make_uint4(L.lo, L.hi, L.u0 | (L.clo ? 0x80000000u : 0u), L.u1 | (L.chi ? 0x80000000u : 0u));
+}
+__device__ __forceinline__ Lane g_lane(const Geo& g, uint32_t c) {
+    if (!g.lanes) return g_lane_slow(g, c);
+    const uint4 x = g.lanes[c];
+    Lane L;
+    L.lo = x.x;
+    L.hi = x.y;
+    L.u0 = x.z & 0x7fffffffu;
+    L.u1 = x.w & 0x7fffffffu;
+    L.clo = (x.z >> 31) != 0;
+    L.chi = (x.w >> 31) != 0;
     return L;
 }
 
@@ -264,14 +282,22 @@ __device__ __forceinline__ uint32_t lane_bucket(const Geo& g, uint32_t c) {
     return (uint32_t)(LANE_NB - 1) - min<uint32_t>(len >> 5, LANE_NB - 1);
 }
 
-constexpr uint32_t LANE_SORT_CHUNK = 4096;         // lanes per workgroup (few global reservations)
+constexpr uint32_t LANE_SORT_CHUNK = 1024;         // lanes per workgroup (4 per thread; ~1k workgroups at config 2)
 
-__global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __restrict__ bucket_cnt) {
+// also records every lane's geometry (g.lanes is null here; later kernels read the records)
+__global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __restrict__ bucket_cnt,
+                                                    uint4* __restrict__ lanes) {
     __shared__ uint32_t h[LANE_NB];
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
     __syncthreads();
     const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK, c1 = min(c0 + LANE_SORT_CHUNK, g.n_chunks);
-    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) atomicAdd(&h[lane_bucket(g, c)], 1u);
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+        const Lane L = g_lane_slow(g, c);
+        lanes[c] = lane_pack(L);
+        const uint32_t len = L.hi - min(L.lo, L.hi);
+        const uint32_t bk = (uint32_t)(LANE_NB - 1) - min(len >> 5, (uint32_t)(LANE_NB - 1));
+        atomicAdd(&h[bk], 1u);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
         if (h[i]) atomicAdd(&bucket_cnt[i], h[i]);
@@ -771,48 +797,120 @@ __device__ __forceinline__ SegV seg_combine(SegV a, SegV b) {
     return r;
 }
 
-__global__ __launch_bounds__(CTX_BLOCK) void k_ctx_scan(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
-                                                        const int32_t* __restrict__ kw, uint32_t n_utt, uint32_t n_slots,
-                                                        uint32_t* __restrict__ incl, int32_t* __restrict__ agg_v,
-                                                        uint32_t* __restrict__ agg_f, uint32_t* __restrict__ stamp,
-                                                        uint32_t epoch, uint32_t* __restrict__ err) {
-    __shared__ SegV wsum[CTX_BLOCK / 64];
-    const uint32_t u = blockIdx.x * CTX_BLOCK + threadIdx.x;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    SegV x;
-    x.f = 0;
-    x.v = -1;
-    if (u < n_utt) {
-        const uint32_t sl = slot[u];
-        if (sl >= n_slots) atomicOr(err, (uint32_t)ERR_SLOT);
-        const bool start = (u == 0) || slot[u - 1] != sl;
-        x.f = start ? 1u : 0u;
-        x.v = (role[u] == PII_ROLE_AGENT && kw[u] >= 0) ? (int32_t)u : -1;
-        if (start && sl < n_slots) {
-            const uint32_t old = atomicExch(&stamp[sl], epoch);
-            if (old == epoch) atomicOr(err, (uint32_t)ERR_ORDER);
+// Two passes over tiles of CTX_TILE rows, CTX_ITEMS consecutive rows per thread (all loads of a thread
+// issued together): k_ctx_scan reduces each tile to its aggregate (and checks slots / ORDER);
+// k_ctx_apply takes the tile's carry from the aggregates before it, re-scans the tile and applies the
+// context per row.  No per-row scan values round-trip HBM.
+constexpr int CTX_ITEMS = 8;
+constexpr int CTX_THREADS = 256;
+constexpr uint32_t CTX_TILE = CTX_ITEMS * CTX_THREADS;
+static_assert(CTX_ITEMS == 8, "ctx_load's vector path reads 8 rows");
+
+// the thread's rows [u0, u0 + CTX_ITEMS) clipped to n_utt: slot of row u0 - 1 .. u0 + CTX_ITEMS.
+// VEC: slot / role are 16 / 8-byte aligned (host checked), so a full group is read with 16-byte loads
+struct CtxRows {
+    uint32_t sl[CTX_ITEMS + 2];      // sl[k + 1] = slot[u0 + k]; sl[0] = slot[u0 - 1]; past n_utt: ~0
+    uint8_t role[CTX_ITEMS];
+    int32_t kw[CTX_ITEMS];
+};
+template <bool VEC>
+__device__ __forceinline__ void ctx_load(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
+                                         const int32_t* __restrict__ kw, uint32_t n_utt, uint32_t u0, CtxRows& r) {
+    r.sl[0] = u0 > 0 && u0 <= n_utt ? slot[u0 - 1] : 0xffffffffu;
+    if (VEC && u0 + CTX_ITEMS <= n_utt) {
+        const uint4 s0 = *reinterpret_cast<const uint4*>(slot + u0), s1 = *reinterpret_cast<const uint4*>(slot + u0 + 4);
+        const uint2 ro = *reinterpret_cast<const uint2*>(role + u0);
+        const int4 k0 = *reinterpret_cast<const int4*>(kw + u0), k1 = *reinterpret_cast<const int4*>(kw + u0 + 4);
+        r.sl[1] = s0.x; r.sl[2] = s0.y; r.sl[3] = s0.z; r.sl[4] = s0.w;
+        r.sl[5] = s1.x; r.sl[6] = s1.y; r.sl[7] = s1.z; r.sl[8] = s1.w;
+        r.sl[9] = u0 + CTX_ITEMS < n_utt ? slot[u0 + CTX_ITEMS] : 0xfffffffeu;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r.role[k] = (uint8_t)(ro.x >> (8 * k));
+            r.role[k + 4] = (uint8_t)(ro.y >> (8 * k));
         }
+        r.kw[0] = k0.x; r.kw[1] = k0.y; r.kw[2] = k0.z; r.kw[3] = k0.w;
+        r.kw[4] = k1.x; r.kw[5] = k1.y; r.kw[6] = k1.z; r.kw[7] = k1.w;
+        return;
     }
+#pragma unroll
+    for (int k = 0; k <= CTX_ITEMS; ++k) r.sl[k + 1] = u0 + k < n_utt ? slot[u0 + k] : 0xfffffffeu;
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k) {
+        const bool in = u0 + k < n_utt;
+        r.role[k] = in ? role[u0 + k] : 0;
+        r.kw[k] = in ? kw[u0 + k] : -1;
+    }
+}
+__device__ __forceinline__ bool ctx_start(const CtxRows& r, uint32_t u0, int k) {
+    return (u0 + k == 0) || r.sl[k] != r.sl[k + 1];
+}
+__device__ __forceinline__ SegV ctx_row(const CtxRows& r, uint32_t u0, int k) {
+    SegV x;
+    x.f = ctx_start(r, u0, k) ? 1u : 0u;
+    x.v = (r.role[k] == PII_ROLE_AGENT && r.kw[k] >= 0) ? (int32_t)(u0 + k) : -1;
+    return x;
+}
+
+// exclusive scan of one SegV per thread over the workgroup (prefix of thread 0 = identity)
+__device__ __forceinline__ SegV ctx_block_excl(SegV x, SegV* wsum, SegV& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    SegV in = x;
+#pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         SegV o;
-        o.f = __shfl_up(x.f, d);
-        o.v = __shfl_up(x.v, d);
-        if (lane >= d) x = seg_combine(o, x);
+        o.f = __shfl_up(in.f, d);
+        o.v = __shfl_up(in.v, d);
+        if (lane >= d) in = seg_combine(o, in);
     }
-    if (lane == 63) wsum[wid] = x;
+    if (lane == 63) wsum[wid] = in;
     __syncthreads();
+    SegV pre{0, -1};
+    for (int w = 0; w < wid; ++w) pre = seg_combine(pre, wsum[w]);
+    total = pre;
+    for (int w = wid; w < CTX_THREADS / 64; ++w) total = seg_combine(total, wsum[w]);
+    SegV ex;
+    ex.f = __shfl_up(in.f, 1);
+    ex.v = __shfl_up(in.v, 1);
+    if (lane == 0) ex = SegV{0, -1};
+    return seg_combine(pre, ex);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(CTX_THREADS) void k_ctx_scan(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
+                                                          const int32_t* __restrict__ kw, uint32_t n_utt, uint32_t n_slots,
+                                                          int32_t* __restrict__ agg_v, uint32_t* __restrict__ agg_f,
+                                                          uint32_t* __restrict__ stamp, uint32_t epoch,
+                                                          uint32_t* __restrict__ err) {
+    __shared__ SegV wsum[CTX_THREADS / 64];
+    const uint32_t u0 = blockIdx.x * CTX_TILE + threadIdx.x * CTX_ITEMS;
+    CtxRows r;
+    ctx_load<VEC>(slot, role, kw, n_utt, u0, r);
+    SegV x{0, -1};
+    bool bad = false, order = false;
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k) {
+        if (u0 + k >= n_utt) break;
+        const uint32_t sl = r.sl[k + 1];
+        bad |= sl >= n_slots;
+        if (ctx_start(r, u0, k) && sl < n_slots) order |= atomicExch(&stamp[sl], epoch) == epoch;
+        x = seg_combine(x, ctx_row(r, u0, k));
+    }
+    if (__any(bad)) {
+        if ((threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_SLOT);
+    }
+    if (__any(order)) {
+        if ((threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_ORDER);
+    }
+    SegV total;
+    (void)ctx_block_excl(x, wsum, total);
     if (threadIdx.x == 0) {
-        for (int w = 1; w < CTX_BLOCK / 64; ++w) wsum[w] = seg_combine(wsum[w - 1], wsum[w]);
-    }
-    __syncthreads();
-    if (wid > 0) x = seg_combine(wsum[wid - 1], x);
-    if (u < n_utt) incl[u] = (x.f ? 0x80000000u : 0u) | (uint32_t)(x.v + 1);
-    if (threadIdx.x == CTX_BLOCK - 1 || u == n_utt - 1) {
-        agg_v[blockIdx.x] = x.v;
-        agg_f[blockIdx.x] = x.f;
+        agg_v[blockIdx.x] = total.v;
+        agg_f[blockIdx.x] = total.f;
     }
 }
 
+// latest hit of the run that continues into tile blk from the tiles before it (-1: none)
 __device__ __forceinline__ int32_t ctx_carry(const int32_t* agg_v, const uint32_t* agg_f, int64_t blk) {
     for (int64_t b = blk - 1; b >= 0; --b) {
         if (agg_v[b] >= 0) return agg_v[b];
@@ -821,68 +919,138 @@ __device__ __forceinline__ int32_t ctx_carry(const int32_t* agg_v, const uint32_
     return -1;
 }
 
-__global__ void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
-                            const int32_t* __restrict__ kw, const int64_t* __restrict__ ts, uint32_t n_utt,
-                            uint32_t n_slots, int64_t ttl_us, const uint32_t* __restrict__ incl,
-                            const int32_t* __restrict__ agg_v, const uint32_t* __restrict__ agg_f,
-                            const int32_t* __restrict__ st_group, const int64_t* __restrict__ st_ts,
-                            int16_t* __restrict__ ctx, int32_t* __restrict__ commit,
-                            int16_t* __restrict__ win_ctx) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n_utt) return;
-    const uint32_t sl = slot[u];
-    const int64_t blk = u / CTX_BLOCK;
-    const bool start = (u == 0) || slot[u - 1] != sl;
-    // hit strictly before u in the same run
-    int32_t prev = -1;
-    if (!start) {
-        const uint32_t pv = incl[u - 1];
-        const bool same_blk = (u % CTX_BLOCK) != 0;
-        prev = same_blk ? (int32_t)(pv & 0x7fffffffu) - 1 : -1;
-        const bool run_started_in_blk = same_blk && (pv & 0x80000000u);
-        if (prev < 0 && !run_started_in_blk) prev = ctx_carry(agg_v, agg_f, blk);
+// Per row: the context a CUSTOMER row uses (the latest AGENT hit before it in the same run, else the
+// stored record, under the TTL), an AGENT row's own group; the last row of each run records the latest
+// hit of the run (commit[u]) and appends u to the commit list (clist, *ncommit; read by k_ctx_commit).
+template <bool VEC>
+__global__ __launch_bounds__(CTX_THREADS) void k_ctx_apply(const uint32_t* __restrict__ slot, const uint8_t* __restrict__ role,
+                                                           const int32_t* __restrict__ kw, const int64_t* __restrict__ ts,
+                                                           uint32_t n_utt, uint32_t n_slots, int64_t ttl_us,
+                                                           const int32_t* __restrict__ agg_v, const uint32_t* __restrict__ agg_f,
+                                                           const int32_t* __restrict__ st_group, const int64_t* __restrict__ st_ts,
+                                                           int16_t* __restrict__ ctx, int32_t* __restrict__ commit,
+                                                           uint32_t* __restrict__ clist, uint32_t* __restrict__ ncommit,
+                                                           int16_t* __restrict__ win_ctx) {
+    __shared__ SegV wsum[CTX_THREADS / 64];
+    __shared__ int32_t s_carry;
+    __shared__ uint32_t s_n, s_base;
+    if (threadIdx.x == 0) {
+        s_carry = ctx_carry(agg_v, agg_f, blockIdx.x);
+        s_n = 0;
     }
-    const uint8_t r = role[u];
-    int16_t used = -1, live = -1;
-    if ((r == PII_ROLE_CUSTOMER || win_ctx) && sl < n_slots) {
-        int32_t g;
-        int64_t t;
-        if (prev >= 0) {
-            g = kw[prev];
-            t = ts ? ts[prev] : 0;
-        } else {
-            g = st_group[sl];
-            t = st_ts[sl];
+    const uint32_t u0 = blockIdx.x * CTX_TILE + threadIdx.x * CTX_ITEMS;
+    CtxRows r;
+    ctx_load<VEC>(slot, role, kw, n_utt, u0, r);
+    SegV x{0, -1};
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k)
+        if (u0 + k < n_utt) x = seg_combine(x, ctx_row(r, u0, k));
+    SegV total;
+    SegV run = ctx_block_excl(x, wsum, total);      // (the barrier inside also publishes s_carry)
+    run = seg_combine(SegV{0, s_carry}, run);
+    uint32_t lastm = 0;                                // bit k: row u0 + k ends a run (commit list)
+    const bool full = VEC && u0 + CTX_ITEMS <= n_utt;
+    int64_t tsv[CTX_ITEMS];
+    if (full && ts) {
+#pragma unroll
+        for (int k = 0; k < CTX_ITEMS / 2; ++k) {
+            const longlong2 t2 = *reinterpret_cast<const longlong2*>(ts + u0 + 2 * k);
+            tsv[2 * k] = t2.x;
+            tsv[2 * k + 1] = t2.y;
         }
-        const int64_t now = ts ? ts[u] : 0;
-        if (g >= 0 && (ts == nullptr || now - t < ttl_us)) live = (int16_t)g;
-        if (r == PII_ROLE_CUSTOMER) used = live;
     }
-    // the re-scan window of row u uses the context a request right after u would GET (main.py:403):
-    // an AGENT row's own hit, else the live record
-    if (win_ctx) win_ctx[u] = (r == PII_ROLE_AGENT && kw[u] >= 0) ? (int16_t)kw[u] : live;
-    ctx[u] = (r == PII_ROLE_AGENT) ? (int16_t)kw[u] : used;
-    // last row of the run: the latest hit of the whole run (to be committed)
-    const bool last = (u == n_utt - 1) || slot[u + 1] != sl;
-    if (last) {
-        int32_t full = (r == PII_ROLE_AGENT && kw[u] >= 0) ? (int32_t)u : prev;
-        commit[u] = full;
+    int16_t cv[CTX_ITEMS], wv[CTX_ITEMS];
+    // pass 1: each row's "latest hit strictly before it in the same run"; pass 2 issues every row's
+    // record loads together (kw/ts of that hit, else the stored record), pass 3 decides
+    int32_t prv[CTX_ITEMS];
+    uint32_t need = 0;
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k) {
+        prv[k] = ctx_start(r, u0, k) ? -1 : run.v;
+        if (u0 + k < n_utt) run = seg_combine(run, ctx_row(r, u0, k));
+        if (u0 + k < n_utt && (r.role[k] == PII_ROLE_CUSTOMER || win_ctx) && r.sl[k + 1] < n_slots) need |= 1u << k;
+    }
+    int32_t gg[CTX_ITEMS];
+    int64_t tt[CTX_ITEMS];
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k) {
+        gg[k] = -1;
+        tt[k] = 0;
+        if ((need >> k) & 1u) {
+            if (prv[k] >= 0) {
+                gg[k] = kw[prv[k]];
+                tt[k] = ts ? ts[prv[k]] : 0;
+            } else {
+                gg[k] = st_group[r.sl[k + 1]];
+                tt[k] = st_ts[r.sl[k + 1]];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < CTX_ITEMS; ++k) {
+        const uint32_t u = u0 + k;
+        if (u >= n_utt) break;
+        const uint32_t sl = r.sl[k + 1];
+        const int32_t prev = prv[k];
+        const uint8_t ro = r.role[k];
+        const int32_t kwu = r.kw[k];
+        int16_t used = -1, live = -1;
+        if ((need >> k) & 1u) {
+            const int64_t now = ts ? (full ? tsv[k] : ts[u]) : 0;
+            if (gg[k] >= 0 && (ts == nullptr || now - tt[k] < ttl_us)) live = (int16_t)gg[k];
+            if (ro == PII_ROLE_CUSTOMER) used = live;
+        }
+        // the re-scan window of row u uses the context a request right after u would GET (main.py:403):
+        // an AGENT row's own hit, else the live record
+        wv[k] = (ro == PII_ROLE_AGENT && kwu >= 0) ? (int16_t)kwu : live;
+        cv[k] = (ro == PII_ROLE_AGENT) ? (int16_t)kwu : used;
+        if (!full) {
+            if (win_ctx) win_ctx[u] = wv[k];
+            ctx[u] = cv[k];
+        }
+        // last row of the run: the latest hit of the whole run (to be committed)
+        const bool last = (u == n_utt - 1) || r.sl[k + 2] != sl;
+        if (last && sl < n_slots) {
+            commit[u] = (ro == PII_ROLE_AGENT && kwu >= 0) ? (int32_t)u : prev;
+            lastm |= 1u << k;
+        }
+    }
+    if (full) {
+        auto pack = [](const int16_t (&a)[CTX_ITEMS]) {
+            return make_uint4((uint16_t)a[0] | (uint32_t)(uint16_t)a[1] << 16, (uint16_t)a[2] | (uint32_t)(uint16_t)a[3] << 16,
+                              (uint16_t)a[4] | (uint32_t)(uint16_t)a[5] << 16, (uint16_t)a[6] | (uint32_t)(uint16_t)a[7] << 16);
+        };
+        *reinterpret_cast<uint4*>(ctx + u0) = pack(cv);
+        if (win_ctx) *reinterpret_cast<uint4*>(win_ctx + u0) = pack(wv);
+    }
+    const uint32_t nmine = (uint32_t)__builtin_popcount(lastm);
+    uint32_t at = nmine ? atomicAdd(&s_n, nmine) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) s_base = atomicAdd(ncommit, s_n);
+    __syncthreads();
+    at += s_base;
+    while (lastm) {
+        clist[at++] = u0 + (uint32_t)__builtin_ctz(lastm);
+        lastm &= lastm - 1u;
     }
 }
 
-__global__ void k_ctx_commit(const uint32_t* __restrict__ slot, const int32_t* __restrict__ kw,
-                             const int64_t* __restrict__ ts, uint32_t n_utt, uint32_t n_slots,
-                             const int32_t* __restrict__ commit, const uint32_t* __restrict__ err,
-                             int32_t* __restrict__ st_group, int64_t* __restrict__ st_ts) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n_utt || *err != 0) return;
-    const uint32_t sl = slot[u];
-    const bool last = (u == n_utt - 1) || slot[u + 1] != sl;
-    if (!last || sl >= n_slots) return;
-    const int32_t j = commit[u];
-    if (j >= 0) {
-        st_group[sl] = kw[j];
-        st_ts[sl] = ts ? ts[j] : 0;
+// write the batch's context back (only when the whole call succeeded): one entry per conversation run
+__global__ __launch_bounds__(256) void k_ctx_commit(const uint32_t* __restrict__ slot, const int32_t* __restrict__ kw,
+                                                    const int64_t* __restrict__ ts, const uint32_t* __restrict__ clist,
+                                                    const uint32_t* __restrict__ ncommit,
+                                                    const int32_t* __restrict__ commit, const uint32_t* __restrict__ err,
+                                                    int32_t* __restrict__ st_group, int64_t* __restrict__ st_ts) {
+    if (*err != 0) return;
+    const uint32_t n = *ncommit;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t u = clist[k];
+        const uint32_t sl = slot[u];
+        const int32_t j = commit[u];
+        if (j >= 0) {
+            st_group[sl] = kw[j];
+            st_ts[sl] = ts ? ts[j] : 0;
+        }
     }
 }
 
@@ -943,6 +1111,15 @@ struct FirstCont {     // a FIRST run still alive after its first window
     int32_t pos;       // next byte, relative to the utterance start
     int32_t last;
 };
+// what k_select reads of a matched pair, written by k_pair_eval next to the likelihood it computed
+// (it lives in the continuation queue, free once k_pair_first is done; one 16-byte load instead of the pair record and then its event record)
+struct SelRec {
+    uint32_t u;        // utterance
+    int32_t ps;        // start, relative to the utterance start
+    uint32_t p;        // detector pattern
+    int32_t lik;       // likelihood after validation + hotwords; -1 = invalid
+};
+static_assert(sizeof(SelRec) == sizeof(FirstCont), "SelRec aliases the FirstCont queue");
 
 // Each wavefront first stages the offsets (u32, batch relative) and roles of the utterances its 64
 // lanes cover into LDS with coalesced loads, so the per-lane walks (event -> utterance) read LDS
@@ -1364,7 +1541,7 @@ __device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ i
 // `cont`.  The workgroup then finishes all its continuations densely, so one long run no longer holds
 // 63 idle lanes; their matches are appended through LDS counters.
 template <bool GI>
-__global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
+__global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
                                                            const uint8_t* __restrict__ text0,
                                                            const uint64_t* __restrict__ offs,
                                                            const unsigned long long* __restrict__ pair_count,
@@ -1451,7 +1628,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_first(const uint4* __restri
 
 // per matched pair: validator + hotword windows of the row's context variant -> likelihood
 template <bool GI>
-__global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
+__global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
                                                           const uint8_t* __restrict__ text0,
                                                           const uint64_t* __restrict__ offs,
                                                           const uint8_t* __restrict__ role,
@@ -1461,7 +1638,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
                                                           const uint32_t* __restrict__ mcount, uint32_t nseg,
                                                           const EvLoc* __restrict__ evloc,
                                                           const int32_t* __restrict__ pend,
-                                                          PairRes* __restrict__ pres) {
+                                                          const PairRes* __restrict__ pres, SelRec* __restrict__ sel) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
@@ -1520,7 +1697,12 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_pair_eval(const uint4* __restric
                     }
                 }
             }
-            pres[i].lik = (int16_t)lik;
+            SelRec r;
+            r.u = Lc.u;
+            r.ps = s;
+            r.p = P.p;
+            r.lik = lik;
+            sel[i] = r;
         }
     }
 }
@@ -1572,8 +1754,7 @@ struct SelTabs {
 struct SelIO {
     const uint64_t* lane_pair;
     const uint32_t* lane_np;
-    const EvLoc* evloc;
-    const PairRes* pres;
+    const SelRec* sel;
     const int32_t* pend;
     uint64_t pair_cap;
     const uint8_t* role;
@@ -1609,7 +1790,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     uint2* __restrict__ spill = io.spill + io.lane_pair[c0];
     // per-utterance state
     uint32_t u = 0xffffffffu;
-    int v = 0, minlik = 0, L = 0;
+    int v = 0, minlik = 0;
     int lp[LIVE], le[LIVE];
     uint32_t n_spill = 0;
     bool spilled = false;
@@ -1657,21 +1838,19 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
         best_e = -1;
     };
     auto flush_utt = [&]() {
-        if (nf_u) io.out_len[u] = (uint32_t)(L + delta_u);
+        if (nf_u) io.out_len[u] += (uint32_t)delta_u;      // (k_chunk_index wrote the row length)
     };
     auto pair = [&](uint64_t i, int e) {
-        const PairRes P = io.pres[i];
-        const EvLoc Lc = io.evloc[P.ev];
-        const int ps = (int)(Lc.s - Lc.ustart);
-        if (Lc.u != u) {
+        const SelRec P = io.sel[i];
+        const int ps = P.ps;
+        if (P.u != u) {
             if (u != 0xffffffffu) {
                 flush_start();
                 flush_utt();
             }
-            u = Lc.u;
+            u = P.u;
             v = (io.role[u] == PII_ROLE_CUSTOMER && io.ctx[u] >= 0) ? io.ctx[u] + 1 : 0;
             minlik = Tb.vmin[v];
-            L = (int)(Lc.uend - Lc.ustart);
 #pragma unroll
             for (int q = 0; q < LIVE; ++q) {
                 lp[q] = -1;
@@ -1978,25 +2157,52 @@ __device__ uint64_t block_exscan(uint64_t (&v)[SCAN_ITEMS], uint64_t* sh) {
     return total;
 }
 
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
-                                                     uint64_t* __restrict__ bsum) {
-    __shared__ uint64_t sh[4];
-    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
-    uint64_t s = 0;
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const uint64_t idx = base + (uint64_t)i * 256 + threadIdx.x;
-        if (idx < n) s += in[idx];
+// Up to two independent scans per launch (blockIdx.y picks one: the two per-lane scans of the front go
+// together); a thread owns SCAN_ITEMS consecutive entries, read / written with 16-byte accesses when
+// the arrays allow it.
+struct ScanArgs {
+    const uint32_t* in[2];
+    uint64_t* out[2];
+    uint32_t n[2];
+    uint32_t bstride;            // block sums of scan 1 at bsum + bstride
+};
+
+__device__ __forceinline__ void scan_load(const uint32_t* __restrict__ in, uint32_t n, uint64_t i0,
+                                          uint32_t (&v)[SCAN_ITEMS]) {
+    if (i0 + SCAN_ITEMS <= n && ((uintptr_t)(in + i0) & 15) == 0) {
+        const uint4 a = *reinterpret_cast<const uint4*>(in + i0), b = *reinterpret_cast<const uint4*>(in + i0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = i0 + i < n ? in[i0 + i] : 0u;
     }
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const ScanArgs a, uint64_t* __restrict__ bsum) {
+    __shared__ uint64_t sh[4];
+    const int y = blockIdx.y;
+    const uint32_t n = a.n[y];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    if (base >= n && blockIdx.x > 0) return;
+    uint32_t v[SCAN_ITEMS];
+    scan_load(a.in[y], n, base + (uint64_t)threadIdx.x * SCAN_ITEMS, v);
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) s += v[i];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     s = wave_incl_scan(s, lane);
     if (lane == 63) sh[wid] = s;
     __syncthreads();
-    if (threadIdx.x == 0) bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+    if (threadIdx.x == 0) bsum[y * a.bstride + blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
-// single block: exclusive scan of nb block sums in place (serial over 256-thread chunks)
-__global__ __launch_bounds__(256) void k_scan_blocks(uint64_t* __restrict__ bsum, uint32_t nb) {
+// one workgroup per scan: exclusive scan of its block sums in place (serial over tiles)
+__global__ __launch_bounds__(256) void k_scan_blocks(const ScanArgs a, uint64_t* __restrict__ bsum0) {
     __shared__ uint64_t sh[4];
+    const int y = blockIdx.x;
+    uint64_t* __restrict__ bsum = bsum0 + y * a.bstride;
+    const uint32_t nb = (a.n[y] + SCAN_TILE - 1) / SCAN_TILE;
     uint64_t carry = 0;
     for (uint32_t c0 = 0; c0 < nb; c0 += SCAN_TILE) {
         uint64_t v[SCAN_ITEMS];
@@ -2016,22 +2222,34 @@ __global__ __launch_bounds__(256) void k_scan_blocks(uint64_t* __restrict__ bsum
 }
 
 // out[i] = exclusive prefix of in[]; out[n] = total
-__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ in, uint32_t n,
-                                                    const uint64_t* __restrict__ bsum, uint64_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_scan_apply(const ScanArgs a, const uint64_t* __restrict__ bsum) {
     __shared__ uint64_t sh[4];
+    const int y = blockIdx.y;
+    const uint32_t n = a.n[y];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    if (base >= n) {
+        if (base == 0 && threadIdx.x == 0) a.out[y][0] = 0;
+        return;
+    }
+    const uint32_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint64_t i0 = base + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t x[SCAN_ITEMS];
+    scan_load(a.in[y], n, i0, x);
     uint64_t v[SCAN_ITEMS];
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const uint64_t idx = base + threadIdx.x * SCAN_ITEMS + i;
-        v[i] = idx < n ? in[idx] : 0;
-    }
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = x[i];
     block_exscan(v, sh);
-    const uint64_t off = bsum[blockIdx.x];
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const uint64_t idx = base + threadIdx.x * SCAN_ITEMS + i;
-        if (idx < n) out[idx] = v[i] + off;
+    const uint64_t off = bsum[y * a.bstride + blockIdx.x];
+    uint64_t* __restrict__ out = a.out[y];
+    if (i0 + SCAN_ITEMS <= n && ((uintptr_t)(out + i0) & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; i += 2)
+            *reinterpret_cast<ulonglong2*>(out + i0 + i) = make_ulonglong2(v[i] + off, v[i + 1] + off);
+    } else {
+        for (int i = 0; i < SCAN_ITEMS; ++i)
+            if (i0 + i < n) out[i0 + i] = v[i] + off;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = bsum[gridDim.x];
+    if (blockIdx.x == nt - 1 && threadIdx.x == 0) out[n] = bsum[y * a.bstride + nt];
 }
 
 // Single-pass exclusive scan (decoupled look-back): out[i] = in[0] + ... + in[i-1], out[n] = total.
@@ -3336,6 +3554,7 @@ struct pii_engine {
     pii_span* fd = nullptr;
     uint32_t *n_ev = nullptr, *n_find = nullptr, *out_len = nullptr, *incl = nullptr, *agg_f = nullptr;
     uint32_t* first_utt = nullptr;
+    uint4* lane_geo = nullptr;         // per lane geometry (Geo::lanes)
     uint32_t* lane_perm = nullptr;     // k_scan slot -> lane (longest lanes first)
     uint32_t* lane_pos = nullptr;      // lane -> slot
     uint32_t* lane_bkt = nullptr;      // [2 * LANE_NB] bucket counts + reservation cursors
@@ -3378,7 +3597,8 @@ struct pii_engine {
     uint64_t *span_offs = nullptr, *bsum = nullptr, *out_offs_tmp = nullptr;
     unsigned long long *lb_state = nullptr, *lb_ticket = nullptr;   // single-pass scan tiles / ticket counter
     uint32_t lb_cap = 0, lb_epoch = 0;
-    uint32_t* d_err = nullptr;
+    uint32_t* d_err = nullptr;            // counter block (one memset per call): err, long_count, ncommit, pair_count
+    uint32_t* ncommit = nullptr;          // k_ctx_apply's commit-list length
     uint64_t* d_totals = nullptr;
     uint64_t* h_totals = nullptr;
     // host-API staging
@@ -3498,6 +3718,7 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         if ((rc = grow(e, e->lane_st, 2 * nl * e->n_sg))) return rc;
         if ((rc = grow(e, e->lane_nf, nl))) return rc;
         if ((rc = grow(e, e->lane_rd, nl))) return rc;
+        if ((rc = grow(e, e->lane_geo, nl))) return rc;
         if ((rc = grow(e, e->lane_reach, nl))) return rc;
         if ((rc = grow(e, e->lane_rowbase, nl))) return rc;
         if ((rc = grow(e, e->dirty, nl))) return rc;
@@ -3527,7 +3748,7 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
     }
     if (e->cap_bsum == 0) {   // scan block sums: the utterance scans and the per-lane pair-count scan
         const size_t n = std::max<size_t>(e->cap_utt, e->cap_lanes);
-        if ((rc = grow(e, e->bsum, n / SCAN_TILE + 2))) return rc;
+        if ((rc = grow(e, e->bsum, 2 * (n / SCAN_TILE + 4)))) return rc;     // two scans per launch
         e->cap_bsum = n;
     }
     return rc;
@@ -3554,17 +3775,22 @@ int ensure_redact(pii_engine* e, uint64_t span_cap, uint64_t out_cap) {
 // each other (the look-back's cross-XCD hand-offs chain up over thousands of tiles: 0.4 ms vs 0.06).
 constexpr uint32_t LB_MAX_TILES = 64;
 
-int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out, hipStream_t st) {
+int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out, hipStream_t st,
+                   const uint32_t* in2 = nullptr, uint32_t n2 = 0, uint64_t* out2 = nullptr) {
     const uint32_t nb = (n + LB_TILE - 1) / LB_TILE;
-    if (nb == 0) {
+    if (in2 == nullptr && nb == 0) {
         HIPCHK(hipMemsetAsync(out, 0, sizeof(uint64_t), st));
         return PII_OK;
     }
-    if (nb > LB_MAX_TILES) {
-        const uint32_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
-        k_scan_reduce<<<nt, 256, 0, st>>>(in, n, e->bsum);
-        k_scan_blocks<<<1, 256, 0, st>>>(e->bsum, nt);
-        k_scan_apply<<<nt, 256, 0, st>>>(in, n, e->bsum, out);
+    if (in2 != nullptr || nb > LB_MAX_TILES) {
+        // reduce / scan-of-sums / apply; a second scan rides along in blockIdx.y
+        ScanArgs a{{in, in2 ? in2 : in}, {out, out2 ? out2 : out}, {n, in2 ? n2 : 0u}, 0};
+        const uint32_t nt = std::max<uint32_t>(1, (std::max(n, a.n[1]) + SCAN_TILE - 1) / SCAN_TILE);
+        a.bstride = nt + 2;
+        const uint32_t ny = in2 ? 2 : 1;
+        k_scan_reduce<<<dim3(nt, ny), 256, 0, st>>>(a, e->bsum);
+        k_scan_blocks<<<ny, 256, 0, st>>>(a, e->bsum);
+        k_scan_apply<<<dim3(nt, ny), 256, 0, st>>>(a, e->bsum);
         HIPCHK(hipGetLastError());
         return PII_OK;
     }
@@ -3615,6 +3841,7 @@ Geo make_geo(const pii_engine* e, const uint64_t* offs, uint32_t n_utt, uint32_t
     Geo g;
     g.offs = offs;
     g.first_utt = e->first_utt;
+    g.lanes = e->lane_geo;
     g.base = base;
     g.n_utt = n_utt;
     g.n_chunks = n_chunks;
@@ -3638,9 +3865,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     const RulesDev& R = e->R;
     e->epoch += 1;
     const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
-    HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(e->pair_count, 0, sizeof(unsigned long long), st));
-    HIPCHK(hipMemsetAsync(e->long_count, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));       // err, long_count, ncommit, pair_count
     HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
@@ -3650,7 +3875,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         if (n_chunks > 0) {
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
-            k_lane_count<<<nsb, 256, 0, st>>>(g, e->lane_bkt);
+            Geo g0 = g;
+            g0.lanes = nullptr;
+            k_lane_count<<<nsb, 256, 0, st>>>(g0, e->lane_bkt, e->lane_geo);
             k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
             // one pass per SCAN group (one for the shipped rules): halo states, scan, stitching; the
             // utterance-start words are written once
@@ -3683,8 +3910,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
                                                                  e->lane_ev, e->lane_np, e->d_err);
             int rc;
-            if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st))) return rc;
-            if ((rc = exclusive_scan(e, multi ? e->lane_evn : e->lane_cnt, n_chunks, e->lane_ev, st))) return rc;
+            if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st, multi ? e->lane_evn : e->lane_cnt,
+                                     n_chunks, e->lane_ev)))
+                return rc;
             if (multi)
                 k_pairs<true, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
@@ -3699,13 +3927,16 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[1], st));
-    const uint32_t nblk = (n_utt + CTX_BLOCK - 1) / CTX_BLOCK;
+    const uint32_t nblk = (uint32_t)(((uint64_t)n_utt + CTX_TILE - 1) / CTX_TILE);
     if (n_utt > 0) {
-        k_ctx_scan<<<nblk, CTX_BLOCK, 0, st>>>(slot, role, e->kw, n_utt, e->n_slots, e->incl, e->agg_v, e->agg_f,
-                                               e->stamp, e->epoch, e->d_err);
-        k_ctx_apply<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, role, e->kw, ts, n_utt, e->n_slots, e->ttl_us,
-                                                         e->incl, e->agg_v, e->agg_f, e->st_group, e->st_ts, ctx,
-                                                         e->commit, win_ctx);
+        // 16-byte row groups when the caller's arrays allow it
+        const bool vec = ((uintptr_t)slot & 15) == 0 && ((uintptr_t)role & 7) == 0 && ((uintptr_t)ts & 15) == 0 &&
+                         ((uintptr_t)ctx & 15) == 0 && ((uintptr_t)win_ctx & 15) == 0;
+        (vec ? k_ctx_scan<true> : k_ctx_scan<false>)<<<nblk, CTX_THREADS, 0, st>>>(
+            slot, role, e->kw, n_utt, e->n_slots, e->agg_v, e->agg_f, e->stamp, e->epoch, e->d_err);
+        (vec ? k_ctx_apply<true> : k_ctx_apply<false>)<<<nblk, CTX_THREADS, 0, st>>>(
+            slot, role, e->kw, ts, n_utt, e->n_slots, e->ttl_us, e->agg_v, e->agg_f, e->st_group, e->st_ts, ctx,
+            e->commit, e->incl, e->ncommit, win_ctx);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
@@ -3751,8 +3982,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
                                                                          st>>>(
             e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
-            e->mcount, e->n_seg, e->evloc, e->pend, e->pres);
-        const SelIO io{e->lane_pair, e->lane_np, e->evloc, e->pres, e->pend, e->pair_cap, role, ctx, e->fd,
+            e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont));
+        const SelIO io{e->lane_pair, e->lane_np, reinterpret_cast<const SelRec*>(e->cont), e->pend, e->pair_cap, role, ctx, e->fd,
                        e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill};
         (e->img_sel.global ? k_select<true> : k_select<false>)<<<(n_chunks + 255) / 256, 256, e->img_sel.lds(), st>>>(
             R, e->img_sel.d, e->img_sel.li, g, io, e->d_err);
@@ -3787,8 +4018,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_hist_reduce<<<dim3(e->hist_types, std::max(1u, std::min(32u, nsb / 256))), 256, 0, st>>>(
                 e->hist_part, nsb, (int)e->hist_types, e->d_err, e->hist);
         }
-        k_ctx_commit<<<(n_utt + 255) / 256, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err,
-                                                          e->st_group, e->st_ts);
+        k_ctx_commit<<<std::min<uint32_t>((n_utt + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
+            slot, e->kw, ts, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
@@ -3886,8 +4117,8 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
             R, W, B, e->wfd, e->wfbase, e->n_wfind, out_offs, e->wspan_offs, e->d_err, out, spans);
         HIPCHK(hipEventRecord(e->kev[3], st));
         k_win_commit<<<(uint32_t)(((uint64_t)n_utt * 16 + 255) / 256), 256, 0, st>>>(W, B, e->wnew, e->d_err);
-        k_ctx_commit<<<nb, 256, 0, st>>>(slot, e->kw, ts, n_utt, e->n_slots, e->commit, e->d_err, e->st_group,
-                                         e->st_ts);
+        k_ctx_commit<<<std::min<uint32_t>(nb, 4 * e->n_cu), 256, 0, st>>>(slot, e->kw, ts, e->incl, e->ncommit,
+                                                                          e->commit, e->d_err, e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
@@ -4293,11 +4524,13 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     const size_t ns = std::max<uint32_t>(1, n_conv_slots);
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
         hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, std::max(R.T, 256) * 8) != hipSuccess ||
-        hipMalloc(&e->long_count, 16) != hipSuccess ||
-        hipMalloc(&e->d_err, 16) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
-        hipMalloc(&e->pair_count, 16) != hipSuccess || hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
+        hipMalloc(&e->d_err, 64) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
+        hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
         hipMemset(e->lb_ticket, 0, 16) != hipSuccess)
         return fail("state allocation failed");
+    e->long_count = e->d_err + 1;
+    e->ncommit = e->d_err + 2;
+    e->pair_count = reinterpret_cast<unsigned long long*>(e->d_err + 4);
     if (hipHostMalloc(&e->h_totals, 64) != hipSuccess) return fail("pinned allocation failed");
     std::vector<int32_t> g(ns, -1);
     if (hipMemcpy(e->st_group, g.data(), ns * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -4314,13 +4547,13 @@ int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->pair_count, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
-                    e->long_rows, e->long_count, e->lane_st, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
+                    e->long_rows, e->lane_st, e->lane_geo, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
                     e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
