@@ -1355,10 +1355,20 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
                                                     uint64_t pair_cap, uint64_t ev_cap,
                                                     const uint64_t* __restrict__ lane_pair,
                                                     const uint64_t* __restrict__ lane_ev,
-                                                    uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err,
+                                                    PairRes* __restrict__ pres) {
     __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
     __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
+    __shared__ uint32_t s_aoff[257];
+    __shared__ uint16_t s_aids[2048];
     if (*err & ERR_ARGS) return;
+    // WRITE: the accept sets' pattern lists (the pair expansion below), staged when small
+    const uint32_t n_dacc = R.n_dacc;
+    const bool small = WRITE && n_dacc < 256 && R.d_acc_off[n_dacc] <= 2048;
+    if (small) {
+        for (uint32_t i = threadIdx.x; i <= n_dacc; i += blockDim.x) s_aoff[i] = R.d_acc_off[i];
+        for (uint32_t i = threadIdx.x; i < R.d_acc_off[n_dacc]; i += blockDim.x) s_aids[i] = R.d_acc_ids[i];
+    }
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t n_chunks = g.n_chunks;
@@ -1442,11 +1452,6 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
         }
         if (act) {
             if (WRITE) {
-                EvPairs ep;
-                ep.first = (uint32_t)(o_top - (o_run + sc));
-                ep.acc = (uint16_t)acc;
-                ep.n = (uint16_t)n;
-                evpairs[E0 + f] = ep;
                 if (n) {
                     EvLoc Lc;
                     Lc.u = u;
@@ -1459,6 +1464,41 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
                 const uint32_t kg = R.k_grp[E.sk];
                 if (kg != (uint32_t)KW_NONE && (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT)
                     atomicMin(reinterpret_cast<unsigned int*>(kw + u), kg);
+            }
+        }
+        if (WRITE) {
+            // the chunk's (start, pattern) pairs, wave-cooperative: numbered 0..tot-1 by a scan of the
+            // events' counts, lane q writes pair q, q + 64, ... (its event found by a 6-step search), so
+            // one store instruction writes neighbouring records (the pair blocks of one lane's events
+            // are adjacent)
+            const uint32_t en = act ? n : 0u;
+            const uint32_t efirst = act ? (uint32_t)(o_top - (o_run + sc)) : 0u;
+            const uint32_t ea0 = en ? (small ? s_aoff[acc] : R.d_acc_off[acc]) : 0u;
+            uint32_t ein = en;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(ein, d);
+                if (lane >= d) ein += o;
+            }
+            const uint32_t etot = __shfl(ein, 63);
+            for (uint32_t q0 = 0; q0 < etot; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const uint32_t v = __shfl(ein, lo + step - 1);
+                    if (v <= q) lo += step;
+                }
+                const uint32_t p_incl = __shfl(ein, lo), p_n = __shfl(en, lo);
+                const uint32_t p_a0 = __shfl(ea0, lo), p_first = __shfl(efirst, lo);
+                if (q < etot) {
+                    const uint32_t i = q - (p_incl - p_n);
+                    PairRes P;
+                    P.ev = (uint32_t)(E0 + f0 + lo);
+                    P.p = small ? s_aids[p_a0 + i] : R.d_acc_ids[p_a0 + i];
+                    P.lik = -1;
+                    pres[p_first + i] = P;
+                }
             }
         }
         // each lane adds its events' pairs of this chunk (the scan value at its last slot here)
@@ -1840,8 +1880,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     auto flush_utt = [&]() {
         if (nf_u) io.out_len[u] += (uint32_t)delta_u;      // (k_chunk_index wrote the row length)
     };
-    auto pair = [&](uint64_t i, int e) {
-        const SelRec P = io.sel[i];
+    auto pair = [&](const SelRec& P, int e) {
         const int ps = P.ps;
         if (P.u != u) {
             if (u != 0xffffffffu) {
@@ -1965,21 +2004,37 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             const int4* pa = reinterpret_cast<const int4*>(io.pend + (pbase - off0));
             const uint32_t ng = (off0 + np + 7u) >> 3;
             int4 q0 = pa[0], q1 = pa[1];
-            for (uint32_t gi = 0; gi < ng; ++gi) {
-                const int4 d0 = q0, d1 = q1;
-                if (gi + 1 < ng) {
-                    const int4* pn = pa + 2 * (gi + 1);
-                    q0 = pn[0];
-                    q1 = pn[1];
+            uint32_t gi = 0, g0 = 0, m = 0;
+            // the next matched pair of the run (false: none left)
+            auto adv = [&](uint32_t& i) -> bool {
+                while (m == 0) {
+                    if (gi >= ng) return false;
+                    const int4 d0 = q0, d1 = q1;
+                    if (gi + 1 < ng) {
+                        const int4* pn = pa + 2 * (gi + 1);
+                        q0 = pn[0];
+                        q1 = pn[1];
+                    }
+                    g0 = 8u * gi;
+                    m = matched_mask8(d0, d1, g0, off0, np);
+                    ++gi;
                 }
-                const uint32_t g0 = 8u * gi;
-                uint32_t m = matched_mask8(d0, d1, g0, off0, np);
-                while (m) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    const uint32_t i = g0 + j - off0;
-                    pair(pbase + i, el[i]);      // (the entry is in L1: its group was just loaded)
-                }
+                const uint32_t j = (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                i = g0 + j - off0;
+                return true;
+            };
+            // each matched pair's SelRec is loaded one pair ahead of its use
+            uint32_t i1 = 0;
+            bool ok = adv(i1);
+            SelRec r1{};
+            if (ok) r1 = io.sel[pbase + i1];
+            while (ok) {
+                const SelRec r = r1;
+                const int e = el[i1];          // (in L1: its group was just loaded)
+                ok = adv(i1);
+                if (ok) r1 = io.sel[pbase + i1];
+                pair(r, e);
             }
         }
         // the pending start and (unless the row continues into the next lane) the utterance end here
@@ -3908,21 +3963,22 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             else
                 k_pairs_flat<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                 e->lane_ev, e->lane_np, e->d_err);
+                                                                 e->lane_ev, e->lane_np, e->d_err, e->pres);
             int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st, multi ? e->lane_evn : e->lane_cnt,
                                      n_chunks, e->lane_ev)))
                 return rc;
-            if (multi)
+            if (multi) {
                 k_pairs<true, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
                                                                  e->lane_evn);
-            else
+                k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
+            } else {
                 k_pairs_flat<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                e->lane_ev, e->lane_np, e->d_err);
-            k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
+                                                                e->lane_ev, e->lane_np, e->d_err, e->pres);
+            }
         }
         HIPCHK(hipGetLastError());
     }
