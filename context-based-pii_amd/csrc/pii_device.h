@@ -64,31 +64,20 @@ __device__ __forceinline__ void shr8(uint4& w) {
 }
 
 // Iterate the bytes of text[lo, hi) in order: BODY sees `c` (the byte) and `i` (its index relative
-// to lo).  The aligned 16-byte chunks holding the range are each loaded once, the next one issued
-// before the current one is stepped (the per-byte DFA chain hides its latency); a runtime loop per
-// byte (a wavefront leaves it as soon as its last lane is done, instead of stepping through whole
-// predicated chunks).
+// to lo).  One window load per 16 bytes, a runtime loop per byte (a wavefront leaves it as soon as
+// its last lane is done, instead of stepping through whole predicated chunks).  (Loading each aligned
+// chunk once with a one-ahead prefetch instead measured 20% slower in k_pair_eval: more VALU, and
+// the prefetch of a run that ends early is wasted.)
 #define PII_FOR_BYTES(text, lo, hi, ...)                                                         \
-    {                                                                                             \
-        const int _lo = (lo), _hi = (hi);                                                         \
-        if (_lo < _hi) {                                                                          \
-            const uintptr_t _s = (uintptr_t)((text) + _lo), _e = (uintptr_t)((text) + _hi);       \
-            uintptr_t _a = _s & ~(uintptr_t)15;                                                   \
-            uint32_t _skip = (uint32_t)(_s - _a);                                                 \
-            uint4 _nx = gload16(_a);                                                              \
-            int i = 0;                                                                            \
-            for (; _a < _e; _a += 16) {                                                           \
-                uint4 _w = _nx;                                                                   \
-                if (_a + 16 < _e) _nx = gload16(_a + 16);                                         \
-                if (_skip) _w = window16(_w, make_uint4(0, 0, 0, 0), _skip);                      \
-                const int _n = (int)((_e - _a < 16 ? _e - _a : 16) - _skip);                      \
-                _skip = 0;                                                                        \
-                for (int _k = 0; _k < _n; ++_k, ++i) {                                            \
-                    const uint32_t c = _w.x & 0xffu;                                              \
-                    __VA_ARGS__;                                                                  \
-                    shr8(_w);                                                                     \
-                }                                                                                 \
-            }                                                                                     \
+    for (int _j = (lo); _j < (hi); _j += 16) {                                                    \
+        const int _n = (hi) - _j < 16 ? (hi) - _j : 16;                                           \
+        uint4 _w = load16((text) + _j, 0, _n);                                                    \
+        for (int _k = 0; _k < _n; ++_k) {                                                         \
+            const uint32_t c = _w.x & 0xffu;                                                      \
+            const int i = _j - (lo) + _k;                                                         \
+            (void)i;                                                                              \
+            __VA_ARGS__;                                                                          \
+            shr8(_w);                                                                             \
         }                                                                                         \
     }
 
@@ -255,6 +244,9 @@ struct Pool {
 // can bound the lockstep cost: first_begin consumes at most one 16-byte window (the byte before s,
 // which picks the start state, then up to 15 bytes) and either finishes or leaves a resumable
 // {state, next position, last match end}; first_resume finishes it.
+#ifndef FIRST_WINDOW
+#define FIRST_WINDOW 16             // the byte before s + 15 steps (at most 16: one window load; 9 measured slower)
+#endif
 struct FirstState {
     uint32_t st;
     int pos;    // next byte to consume
@@ -286,7 +278,9 @@ __device__ __forceinline__ int first_begin(const Pool& pool, const int32_t* d, c
     const uint8_t* cm = pool.cmap + d[2];
     const uint32_t nc = (uint32_t)d[3];
     const int lo = s == 0 ? 0 : s - 1;
-    const int hi = L - lo < 16 ? L : lo + 16;
+    // lockstep window: most runs end within a few bytes (median 5 steps at config 2), so a
+    // wavefront steps FIRST_WINDOW bytes in lockstep and the longer runs continue densely
+    const int hi = L - lo < FIRST_WINDOW ? L : lo + FIRST_WINDOW;
     uint4 w = load16(text + lo, 0, hi - lo > 0 ? hi - lo : 1);
     uint32_t st;
     int j = s;

@@ -3497,6 +3497,11 @@ bool add_dfa(DfaPool& dp, const int32_t* d, const uint16_t* trans, const uint8_t
     if (ns > (int32_t)DFA_STATE_MASK + 1) return false;
     int32_t nd[8];
     std::memcpy(nd, d, sizeof(nd));
+    // LDS bank stagger (32 banks x 4 B): a pair kernel's wavefront runs many patterns' automata over
+    // the same text bytes, so automaton k's transition table starts at bank k mod 32 and its class map
+    // 4 bytes after the previous map's end (byte c of every map would otherwise sit in one bank)
+    const size_t k = dp.desc.size() / 8;
+    while (dp.trans.size() % 64 != (2 * k) % 64) dp.trans.push_back(0);
     nd[0] = (int32_t)dp.trans.size();
     nd[1] = 0;
     nd[2] = (int32_t)dp.cmap.size();
@@ -3505,6 +3510,7 @@ bool add_dfa(DfaPool& dp, const int32_t* d, const uint16_t* trans, const uint8_t
         dp.trans.push_back((uint16_t)(dst | ((flags[d[1] + dst] & 3u) << 14)));
     }
     dp.cmap.insert(dp.cmap.end(), cmap + d[2], cmap + d[2] + 256);
+    dp.cmap.insert(dp.cmap.end(), 4, (uint8_t)0);
     dp.desc.insert(dp.desc.end(), nd, nd + 8);
     return true;
 }
