@@ -426,9 +426,15 @@ def relax_items(items, budget: int):
                 return out, False, 0
             continue
         if op == C.BRANCH:
-            alts = [relax_items(list(b), budget)[0] for b in av[1]]
-            out.append((op, (None, alts)))
-            return out, False, 0
+            # each alternative relaxed with the budget left; when every one of them is taken whole, the
+            # prefix goes on past the alternation (with the smallest budget any alternative left), so a
+            # pattern like (0?[1-9]|1[0-2])/... keeps its '/' instead of firing at every number
+            rs = [relax_items(list(b), budget) for b in av[1]]
+            out.append((op, (None, [r[0] for r in rs])))
+            if not all(r[1] for r in rs):
+                return out, False, 0
+            budget = min(r[2] for r in rs)
+            continue
         if op in (C.MAX_REPEAT, C.MIN_REPEAT):
             lo, hi, sub = av
             sub = list(sub)
@@ -671,6 +677,7 @@ class Pattern:
     likelihood: int
     validator: Optional[str]
     custom: bool
+    scan_prefix: Optional[int] = None     # characters the SCAN prefilter keeps (None: SCAN_BUDGET)
 
 
 @dataclass
@@ -705,7 +712,8 @@ class Rules:
                 continue
             for v in variants:
                 self.patterns.append(Pattern(len(self.patterns), name, v["pattern"],
-                                             lik_value(v.get("likelihood", "POSSIBLE")), v.get("validator"), False))
+                                             lik_value(v.get("likelihood", "POSSIBLE")), v.get("validator"), False,
+                                             v.get("scan_prefix")))
         for c in self.custom_defs:
             name = c["info_type"]["name"]
             if "regex" in c:
@@ -863,9 +871,13 @@ def _table_bytes(m: MealyDFA) -> int:
     return m.n_states * ((m.n_classes + 2) & ~1) * 2
 
 
-def _scan_dfa(patterns: Sequence[Pattern], budget: int, max_bytes: Optional[int] = None) -> Optional[MealyDFA]:
+def _scan_dfa(patterns: Sequence[Pattern], budget: int, max_bytes: Optional[int] = None,
+              prefixes: bool = True) -> Optional[MealyDFA]:
+    """prefixes: honour the detectors' scan_prefix (longer relaxed prefixes: fewer candidate pairs,
+    more states); without, every pattern keeps `budget` characters."""
     nd = NFA()
-    sd = [add_relaxed(nd, p.pattern, p.pid, budget, reverse=True) for p in patterns]
+    sd = [add_relaxed(nd, p.pattern, p.pid, (p.scan_prefix if prefixes else None) or budget, reverse=True)
+          for p in patterns]
     try:
         m = build_mealy_dfa(nd, sd, max_bytes=max_bytes)
     except RuleError:
@@ -873,6 +885,14 @@ def _scan_dfa(patterns: Sequence[Pattern], budget: int, max_bytes: Optional[int]
             raise
         return None
     return m if max_bytes is None or _table_bytes(m) <= max_bytes else None
+
+
+def _scan_dfa_fit(patterns: Sequence[Pattern], budget: int, max_bytes: int) -> Optional[MealyDFA]:
+    """the automaton with the declared scan prefixes, else (too large) with `budget` for every pattern"""
+    m = _scan_dfa(patterns, budget, max_bytes)
+    if m is None and any(p.scan_prefix for p in patterns):
+        m = _scan_dfa(patterns, budget, max_bytes, prefixes=False)
+    return m
 
 
 def _prefix_key(p: Pattern) -> str:
@@ -887,7 +907,7 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
     and excluder pattern; the rest, ordered by prefix so that similar prefixes share states, is cut
     in halves until each half fits."""
     limit0 = SCAN_LDS_BYTES - SCAN_CMAP_BYTES - k_bytes
-    whole = _scan_dfa(rules.patterns, budget, limit0) if len(rules.patterns) <= 256 else None
+    whole = _scan_dfa_fit(rules.patterns, budget, limit0) if len(rules.patterns) <= 256 else None
     if whole is not None:
         return [(list(rules.patterns), whole)]
     excl = set()
@@ -899,13 +919,13 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
                         "info_types", [])}
     base = [p for p in rules.patterns if not p.custom or p.type_name in excl]
     rest = sorted((p for p in rules.patterns if p.custom and p.type_name not in excl), key=_prefix_key)
-    g0 = _scan_dfa(base, budget, limit0)
+    g0 = _scan_dfa_fit(base, budget, limit0)
     if g0 is None:
         raise RuleError("the built-in detectors' SCAN automaton does not fit k_scan's LDS")
     out = [(base, g0)]
 
     def split(pats):
-        m = _scan_dfa(pats, budget, SCAN_GROUP_BYTES)
+        m = _scan_dfa_fit(pats, budget, SCAN_GROUP_BYTES)
         if m is not None:
             out.append((pats, m))
             return

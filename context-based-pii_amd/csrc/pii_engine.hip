@@ -37,7 +37,7 @@ namespace {
 
 constexpr int P_MAX = 64;          // detector patterns handled by k_select's private state
 constexpr int NE_MAX = 2;          // excluder patterns
-constexpr int SCAN_BLOCK = 512;
+constexpr int SCAN_BLOCK = 768;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
 constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
 constexpr int SCAN_ITEMS = 8;      // items per thread in the offset scans (blocked, 16-byte accesses)
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
