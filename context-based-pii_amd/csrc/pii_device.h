@@ -82,86 +82,123 @@ __device__ __forceinline__ void shr8(uint4& w) {
     }
 
 // ---------------------------------------------------------------------------------- validators
-// SURVEY A.1 / B.4, one forward pass over q[0, n).
-__device__ inline bool v_luhn(const uint8_t* q, int n) {
+// SURVEY A.1 / B.4, one forward pass over the match's n bytes, read through a byte source: MemSrc
+// (16-byte windows from memory) or RegSrc (the first 32 bytes, loaded once before the validator
+// dispatch -- a wavefront's lanes run different validators one after another, and loads inside each
+// would serialise one memory latency per validator kind).  src.each(n, f) calls f(byte, index).
+struct MemSrc {
+    const uint8_t* q;
+    template <class F>
+    __device__ __forceinline__ void each(int n, F&& f) const {
+        PII_FOR_BYTES(q, 0, n, { f(c, i); })
+    }
+    __device__ __forceinline__ uint32_t word1() const { return load16(q, 4, 8).y; }    // bytes 4..7
+};
+struct RegSrc {
+    uint4 a, b;                     // bytes [0, 16), [16, 32)
+    template <class F>
+    __device__ __forceinline__ void each(int n, F&& f) const {
+        uint4 w = a;
+        const int m = n < 16 ? n : 16;
+        for (int k = 0; k < m; ++k) {
+            f(w.x & 0xffu, k);
+            shr8(w);
+        }
+        w = b;
+        for (int k = 16; k < n; ++k) {
+            f(w.x & 0xffu, k);
+            shr8(w);
+        }
+    }
+    __device__ __forceinline__ uint32_t word1() const { return a.y; }
+};
+// bytes [q, q + 32) as a register window (only the aligned chunks holding one of the n bytes are read)
+__device__ __forceinline__ RegSrc load32(const uint8_t* q, int n) {
+    const uintptr_t a0 = (uintptr_t)q & ~(uintptr_t)15;
+    const uint32_t off = (uint32_t)((uintptr_t)q - a0);
+    const uintptr_t end = (uintptr_t)q + (uintptr_t)n;
+    uint4 c0 = gload16(a0), c1 = make_uint4(0, 0, 0, 0), c2 = c1;
+    if (a0 + 16 < end) c1 = gload16(a0 + 16);
+    if (a0 + 32 < end) c2 = gload16(a0 + 32);
+    return RegSrc{window16(c0, c1, off), window16(c1, c2, off)};
+}
+
+template <class S>
+__device__ inline bool v_luhn(const S src, int n) {
     // digit k (from the left) is doubled iff (cnt - 1 - k) is odd: keep both parities' sums
     int sa = 0, sb = 0, cnt = 0;
-    PII_FOR_BYTES(q, 0, n, {
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
         if (is_digit(c)) {
+            // (value selects, not branches assigning different variables: those make the compiler
+            // pick the variable's address and keep it in scratch)
             const int d = (int)(c - '0');
             const int dd = d * 2 > 9 ? d * 2 - 9 : d * 2;
-            if (cnt & 1) {
-                sa += dd;
-                sb += d;
-            } else {
-                sa += d;
-                sb += dd;
-            }
+            const bool odd = cnt & 1;
+            sa += odd ? dd : d;
+            sb += odd ? d : dd;
             ++cnt;
         }
-    })
+    });
     const int s = ((cnt - 1) & 1) ? sb : sa;
     return cnt >= 2 && s % 10 == 0;
 }
 
-__device__ inline bool v_nanp(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_nanp(const S src, int n) {
     int k = 0;
     bool ok = true;
-    PII_FOR_BYTES(q, 0, n, {
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
         if (is_digit(c)) {
             if ((k == 0 || k == 3) && c < '2') ok = false;
             ++k;
         }
-    })
+    });
     return ok && k == 10;
 }
 
-__device__ inline bool v_ssn(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_ssn(const S src, int n) {
     int k = 0;
     uint32_t area = 0, group = 0, serial = 0;
-    PII_FOR_BYTES(q, 0, n, {
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
         if (is_digit(c)) {
             const uint32_t d = c - '0';
-            if (k < 3) area = area * 10 + d;
-            else if (k < 5) group = group * 10 + d;
-            else serial = serial * 10 + d;
+            area = k < 3 ? area * 10 + d : area;
+            group = (k >= 3 && k < 5) ? group * 10 + d : group;
+            serial = k >= 5 ? serial * 10 + d : serial;
             ++k;
         }
-    })
+    });
     return k == 9 && area != 0 && area != 666 && area < 900 && group != 0 && serial != 0;
 }
 
-__device__ inline bool v_ein(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_ein(const S src, int n) {
     int k = 0;
     uint32_t p = 0;
-    PII_FOR_BYTES(q, 0, n, {
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
         if (is_digit(c)) {
             if (k < 2) p = p * 10 + (c - '0');
             ++k;
         }
-    })
+    });
     if (k != 9) return false;
     const uint64_t lo = 0xfffdffffcff1fc7eull, hi = 0x0000000cfdff3f9full;   // oracle EIN_PREFIXES
     return p < 64 ? ((lo >> p) & 1) : ((hi >> (p - 64)) & 1);
 }
 
-__device__ inline bool v_ipv4(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_ipv4(const S src, int n) {
     int parts = 0, len = 0;
     uint32_t val = 0;
     bool ok = true;
-    PII_FOR_BYTES(q, 0, n, {
-        if (c == '.') {
-            if (len == 0 || len > 3 || val > 255) ok = false;
-            ++parts;
-            len = 0;
-            val = 0;
-        } else if (is_digit(c)) {
-            val = val * 10 + (c - '0');
-            ++len;
-        } else {
-            ok = false;
-        }
-    })
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
+        const bool dot = c == '.', dig = is_digit(c);
+        ok = ok && !(dot && (len == 0 || len > 3 || val > 255)) && (dot || dig);
+        parts += dot ? 1 : 0;
+        val = dot ? 0u : (dig ? val * 10 + (c - '0') : val);
+        len = dot ? 0 : (dig ? len + 1 : len);
+    });
     if (len == 0 || len > 3 || val > 255) ok = false;     // the final field
     return ok && parts + 1 == 4;
 }
@@ -172,10 +209,11 @@ __constant__ const uint32_t ISO3166_BITS[22] = {0xeedf5978u, 0xdeddbdefu, 0x1584
                               0x538f3c40u, 0x40000001u, 0xfdf15100u, 0x9fbb3ae7u, 0x0410419au, 0x00408557u,
                               0x00004002u, 0x00100000u, 0x00400408u, 0x00000001u};
 
-__device__ inline bool v_swift(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_swift(const S src, int n) {
     if (n != 8 && n != 11) return false;
-    const uint4 w = load16(q, 4, 6);
-    const uint32_t a = ((w.y >> 0) & 0xffu) - 'A', b = ((w.y >> 8) & 0xffu) - 'A';
+    const uint32_t w = src.word1();
+    const uint32_t a = ((w >> 0) & 0xffu) - 'A', b = ((w >> 8) & 0xffu) - 'A';
     if (a >= 26u || b >= 26u) return false;
     const uint32_t i = a * 26 + b;
     return (ISO3166_BITS[i >> 5] >> (i & 31)) & 1;
@@ -183,11 +221,12 @@ __device__ inline bool v_swift(const uint8_t* q, int n) {
 
 // mod-97 of the string rotated by four characters (spaces skipped), in one forward pass:
 // value(chars[4:]) * 10^digits(chars[0:4]) + value(chars[0:4])  (mod 97)
-__device__ inline bool v_iban(const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool v_iban(const S src, int n) {
     int len = 0;
     uint32_t head = 0, headpow = 1, tail = 0;
     bool ok = true;
-    PII_FOR_BYTES(q, 0, n, {
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
         if (c != ' ') {
             uint32_t v, m;
             if (is_digit(c)) {
@@ -201,31 +240,89 @@ __device__ inline bool v_iban(const uint8_t* q, int n) {
                 v = 0;
                 m = 1;
             }
-            if (len < 4) {
-                head = (head * m + v) % 97;
-                headpow = (headpow * m) % 97;
-            } else {
-                tail = (tail * m + v) % 97;
-            }
+            // head / headpow take the first four characters (< 100^4 < 2^27: no reduction needed);
+            // tail is reduced only when it could overflow (one modulo per few characters)
+            const bool h4 = len < 4;
+            head = h4 ? head * m + v : head;
+            headpow = h4 ? headpow * m : headpow;
+            uint32_t t = h4 ? tail : tail * m + v;
+            if (t >= (1u << 24)) t %= 97;
+            tail = t;
             ++len;
         }
-    })
+    });
     if (!ok || len < 15 || len > 34) return false;
-    return (tail * headpow + head) % 97 == 1;
+    return ((tail % 97) * (headpow % 97) + head % 97) % 97 == 1;
 }
 
-__device__ inline bool validate(int id, const uint8_t* q, int n) {
+template <class S>
+__device__ inline bool validate_src(int id, const S src, int n) {
     switch (id) {
         case 0: return true;
-        case 1: return v_luhn(q, n);
-        case 2: return v_nanp(q, n);
-        case 3: return v_ssn(q, n);
-        case 4: return v_ein(q, n);
-        case 5: return v_ipv4(q, n);
-        case 6: return v_swift(q, n);
-        case 7: return v_iban(q, n);
+        case 1: return v_luhn(src, n);
+        case 2: return v_nanp(src, n);
+        case 3: return v_ssn(src, n);
+        case 4: return v_ein(src, n);
+        case 5: return v_ipv4(src, n);
+        case 6: return v_swift(src, n);
+        case 7: return v_iban(src, n);
         default: return false;
     }
+}
+
+// luhn / nanp / ssn / ein / ipv4 in ONE pass: a wavefront whose lanes hold different validators
+// steps the match bytes once instead of once per validator kind (each kind's loop would run with the
+// lanes of the other kinds idle).  Same results as v_luhn ... v_ipv4 (which the IBAN / SWIFT / long
+// paths and the window kernels keep using).
+template <class S>
+__device__ inline bool v_digits(int id, const S src, int n) {
+    int cnt = 0, sa = 0, sb = 0;                  // luhn
+    uint32_t v9 = 0, d0 = 0, d3 = 0;              // the first nine digits as a number; digits 0 and 3
+    int parts = 0, len = 0;                       // ipv4
+    uint32_t val = 0;
+    bool ok4 = true;
+    src.each(n, [&](uint32_t c, int) __attribute__((always_inline)) {
+        const bool dig = is_digit(c), dot = c == '.';
+        const uint32_t d = dig ? c - '0' : 0u;
+        const int dd = d * 2 > 9 ? (int)(d * 2 - 9) : (int)(d * 2);
+        const bool odd = cnt & 1;
+        sa += dig ? (odd ? dd : (int)d) : 0;
+        sb += dig ? (odd ? (int)d : dd) : 0;
+        v9 = (dig && cnt < 9) ? v9 * 10 + d : v9;
+        d0 = (dig && cnt == 0) ? d : d0;
+        d3 = (dig && cnt == 3) ? d : d3;
+        cnt += dig ? 1 : 0;
+        ok4 = ok4 && !(dot && (len == 0 || len > 3 || val > 255)) && (dot || dig);
+        parts += dot ? 1 : 0;
+        val = dot ? 0u : (dig ? val * 10 + d : val);
+        len = dot ? 0 : (dig ? len + 1 : len);
+    });
+    switch (id) {
+        case 1: return cnt >= 2 && (((cnt - 1) & 1) ? sb : sa) % 10 == 0;                  // luhn
+        case 2: return cnt == 10 && d0 >= 2 && d3 >= 2;                                       // nanp
+        case 3: {                                                                             // ssn
+            const uint32_t area = v9 / 1000000u, group = (v9 / 10000u) % 100u, serial = v9 % 10000u;
+            return cnt == 9 && area != 0 && area != 666 && area < 900 && group != 0 && serial != 0;
+        }
+        case 4: {                                                                             // ein
+            if (cnt != 9) return false;
+            const uint32_t p = v9 / 10000000u;
+            const uint64_t lo = 0xfffdffffcff1fc7eull, hi = 0x0000000cfdff3f9full;   // oracle EIN_PREFIXES
+            return p < 64 ? ((lo >> p) & 1) : ((hi >> (p - 64)) & 1);
+        }
+        case 5: return ok4 && !(len == 0 || len > 3 || val > 255) && parts + 1 == 4;        // ipv4
+        default: return false;
+    }
+}
+
+// matches of up to 32 bytes (every shipped validator's but a spaced IBAN's) are read once, up front
+__device__ inline bool validate(int id, const uint8_t* q, int n) {
+    if (id == 0) return true;
+    if (n <= 32) {
+        const RegSrc r = load32(q, n);
+        return (id >= 1 && id <= 5) ? v_digits(id, r, n) : validate_src(id, r, n);
+    }
+    return validate_src(id, MemSrc{q}, n);
 }
 
 // ---------------------------------------------------------------------------------- DFA runners
