@@ -189,9 +189,12 @@ class DeviceBatch:
         self.ctx = torch.empty(self.n, dtype=torch.int16, device=dev)
 
     def run(self, eng):
-        eng.scan_redact_device(self.text.data_ptr(), self.offs.data_ptr(), self.n, self.slot.data_ptr(),
-                               self.role.data_ptr(), self.ts.data_ptr(), self.out.data_ptr(), self.out_cap,
-                               self.out_offs.data_ptr(), self.spans.data_ptr(), self.span_cap, self.ctx.data_ptr())
+        # the batch is resident and its size known: the declared-size entry point enqueues without a
+        # device-to-host read of the offsets (pii_scan_redact_device_ex)
+        eng.scan_redact_device_ex(self.text.data_ptr(), self.offs.data_ptr(), self.n, 0, self.n_bytes,
+                                  self.slot.data_ptr(), self.role.data_ptr(), self.ts.data_ptr(), self.out.data_ptr(),
+                                  self.out_cap, self.out_offs.data_ptr(), self.spans.data_ptr(), self.span_cap,
+                                  self.ctx.data_ptr())
 
 
 def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None, bank=None):

@@ -3661,7 +3661,9 @@ struct pii_engine {
     uint32_t* d_err = nullptr;            // counter block (one memset per call): err, long_count, ncommit, pair_count
     uint32_t* ncommit = nullptr;          // k_ctx_apply's commit-list length
     uint64_t* d_totals = nullptr;
-    uint64_t* h_totals = nullptr;
+    uint64_t* h_totals = nullptr;    // pinned copy of d_totals (+ the histogram behind it)
+    bool h_hist_valid = false;       // h_totals' histogram is the device's as of the last call (no reset since)
+    bool reset_pending = false;      // a histogram reset was enqueued on `stream` and not yet ordered
     // host-API staging
     uint64_t cap_h_bytes = 0, cap_h_out = 0;
     uint32_t cap_h_utt = 0, cap_h_spans = 0;
@@ -3918,12 +3920,17 @@ uint32_t row_grid(const pii_engine* e, uint64_t total_bytes) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_rows, 2 * (uint64_t)e->n_cu));
 }
 
+// d_totals: 8 u64 totals, then the u64[max(T, 256)] per-infoType histogram
+size_t hist_bytes(const pii_engine* e) { return 64 + (size_t)std::max(e->R.T, 256) * 8; }
+
 // The stages every call shares: lane index, reverse DFA scan (+ the stitching of cut rows), (start,
 // pattern) pair queue, context (segmented scan), leftmost-first confirmation.  Records tev[0..2].
 int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint32_t n_chunks,
                  uint64_t base, uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts,
                  int16_t* ctx, int16_t* win_ctx, const unsigned long long* pcount, hipStream_t st) {
     const RulesDev& R = e->R;
+    if (e->reset_pending && st != e->stream) HIPCHK(hipStreamSynchronize(e->stream));   // order the reset
+    e->reset_pending = false;
     e->epoch += 1;
     const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
     HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));       // err, long_count, ncommit, pair_count
@@ -4085,7 +4092,8 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
-    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, hist_bytes(e), hipMemcpyDeviceToHost, st));
+    e->h_hist_valid = true;
     HIPCHK(hipEventRecord(e->tev[6], st));
     return PII_OK;
 }
@@ -4184,7 +4192,8 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
-    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, hist_bytes(e), hipMemcpyDeviceToHost, st));
+    e->h_hist_valid = true;
     HIPCHK(hipEventRecord(e->tev[6], st));
     return PII_OK;
 }
@@ -4585,15 +4594,17 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (hipEventCreate(&t) != hipSuccess) return fail("event");
     const size_t ns = std::max<uint32_t>(1, n_conv_slots);
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
-        hipMalloc(&e->stamp, ns * 4) != hipSuccess || hipMalloc(&e->hist, std::max(R.T, 256) * 8) != hipSuccess ||
-        hipMalloc(&e->d_err, 64) != hipSuccess || hipMalloc(&e->d_totals, 64) != hipSuccess ||
+        hipMalloc(&e->stamp, ns * 4) != hipSuccess ||
+        hipMalloc(&e->d_err, 64) != hipSuccess || hipMalloc(&e->d_totals, hist_bytes(e)) != hipSuccess ||
         hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
         hipMemset(e->lb_ticket, 0, 16) != hipSuccess)
         return fail("state allocation failed");
     e->long_count = e->d_err + 1;
     e->ncommit = e->d_err + 2;
     e->pair_count = reinterpret_cast<unsigned long long*>(e->d_err + 4);
-    if (hipHostMalloc(&e->h_totals, 64) != hipSuccess) return fail("pinned allocation failed");
+    // the histogram lives right after the totals, so one async copy at the end of a call brings both
+    e->hist = reinterpret_cast<unsigned long long*>(e->d_totals + 8);
+    if (hipHostMalloc(&e->h_totals, hist_bytes(e)) != hipSuccess) return fail("pinned allocation failed");
     std::vector<int32_t> g(ns, -1);
     if (hipMemcpy(e->st_group, g.data(), ns * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(e->st_ts, 0, ns * 8) != hipSuccess || hipMemset(e->stamp, 0, ns * 4) != hipSuccess ||
@@ -4608,7 +4619,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
 int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->hist, e->ev, e->fd, e->n_ev, e->n_find,
+    void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->ev, e->fd, e->n_ev, e->n_find,
                     e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
@@ -4973,19 +4984,27 @@ int pii_context_set(pii_engine* e, uint32_t slot, int32_t group, int64_t ts_us) 
 int pii_histogram(pii_engine* e, uint64_t* counts, uint32_t n) {
     if (!e || !counts) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
     const uint32_t T = (uint32_t)e->R.T;
+    if (e->h_hist_valid) {         // the last call copied it with its totals: no extra round trip
+        HIPCHK(hipEventSynchronize(e->tev[6]));
+        const uint64_t* h = e->h_totals + 8;
+        for (uint32_t i = 0; i < n; ++i) counts[i] = i < T ? h[i] : 0;
+        return PII_OK;
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
     std::vector<unsigned long long> h(T);
     if (T) HIPCHK(hipMemcpy(h.data(), e->hist, T * 8, hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < n; ++i) counts[i] = i < T ? h[i] : 0;
     return PII_OK;
 }
 
+// stream-ordered: the next call on the engine's stream starts from zero (no host wait here)
 int pii_histogram_reset(pii_engine* e) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemsetAsync(e->hist, 0, std::max(e->R.T, 256) * 8, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    e->h_hist_valid = false;
+    e->reset_pending = true;
     return PII_OK;
 }
 

@@ -57,6 +57,8 @@ class OracleBenchEngine:
     def scan_redact_device(self, *a):
         self.h += self.counts
 
+    scan_redact_device_ex = scan_redact_device
+
     def sync(self):
         return self.ob, self.ns, 0
 
