@@ -177,34 +177,64 @@ __device__ __forceinline__ void row_lanes(const Geo& g, uint32_t r, uint32_t& ca
 // first_utt[c] = first utterance starting at or after slice c (c in [0, n_chunks]); also writes every
 // row's defaults (no findings: out_len = len; keyword group = the always-present group for AGENT rows,
 // else -1) with coalesced stores, and lists the rows that will be cut (long rows).
-__global__ void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role, uint32_t n_utt,
-                              uint32_t n_chunks, uint32_t lane_shift, uint32_t r0, uint32_t long_min, int kw_always,
-                              uint32_t* __restrict__ first_utt, uint32_t* __restrict__ out_len,
-                              int32_t* __restrict__ kw, uint32_t* __restrict__ wc_n,
-                              uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count,
-                              uint64_t decl_base, uint64_t decl_bytes, uint32_t* __restrict__ err) {
-    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u > n_utt) return;
+constexpr int CI_ROWS = 4;          // rows per thread in k_chunk_index (16-byte row-default stores)
+static_assert(CI_ROWS == 4, "k_chunk_index stores the row defaults as one uint4 / int4");
+__global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role,
+                                                     uint32_t n_utt, uint32_t n_chunks, uint32_t lane_shift, uint32_t r0,
+                                                     uint32_t long_min, int kw_always,
+                                                     uint32_t* __restrict__ first_utt, uint32_t* __restrict__ out_len,
+                                                     int32_t* __restrict__ kw, uint32_t* __restrict__ wc_n,
+                                                     uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count,
+                                                     uint64_t decl_base, uint64_t decl_bytes, uint32_t* __restrict__ err) {
+    const uint32_t u0 = (blockIdx.x * blockDim.x + threadIdx.x) * CI_ROWS;
+    if (u0 > n_utt) return;
     const uint64_t base = offs[0];
     // the caller declared offsets[0] and the batch size (no host round trip): every later kernel sized
     // its work from them, so a wrong declaration stops the call
-    if (u == n_utt && (base != decl_base || offs[n_utt] - base != decl_bytes)) atomicOr(err, (uint32_t)ERR_ARGS);
-    const uint64_t su = offs[u] - base + r0;
-    uint64_t c_lo = 0;
-    if (u > 0) c_lo = ((offs[u - 1] - base + r0) >> lane_shift) + 1;
-    uint64_t c_hi = (u == n_utt) ? n_chunks : su >> lane_shift;
-    if (c_hi > n_chunks) c_hi = n_chunks;
-    for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
-    if (u < n_utt) {
-        const uint64_t len = offs[u + 1] - offs[u];
-        out_len[u] = (uint32_t)len;
-        kw[u] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
-        if (wc_n) wc_n[u] = 0;
-        // a row that some slice boundary cuts (same test as g_cut)
-        if (long_min != NO_CUTS && len > long_min) {
-            const uint64_t k = ((offs[u] - base + r0) >> lane_shift) + 1;      // first boundary after its start
-            if (k < n_chunks && ((int64_t)(k << lane_shift) - (int64_t)r0) < (int64_t)(offs[u + 1] - base))
-                long_rows[atomicAdd(long_count, 1u)] = u;
+    if (u0 + CI_ROWS > n_utt && (base != decl_base || offs[n_utt] - base != decl_bytes)) atomicOr(err, (uint32_t)ERR_ARGS);
+    // offsets of rows u0 - 1 .. u0 + CI_ROWS, issued together
+    uint64_t o[CI_ROWS + 2];
+#pragma unroll
+    for (int k = 0; k < CI_ROWS + 2; ++k) {
+        const int64_t u = (int64_t)u0 - 1 + k;
+        o[k] = (u >= 0 && u <= (int64_t)n_utt) ? offs[u] : 0;
+    }
+    uint32_t ol[CI_ROWS];
+    int32_t kv[CI_ROWS];
+#pragma unroll
+    for (int k = 0; k < CI_ROWS; ++k) {
+        const uint32_t u = u0 + k;
+        if (u > n_utt) break;
+        const uint64_t su = o[k + 1] - base + r0;
+        uint64_t c_lo = 0;
+        if (u > 0) c_lo = ((o[k] - base + r0) >> lane_shift) + 1;
+        uint64_t c_hi = (u == n_utt) ? n_chunks : su >> lane_shift;
+        if (c_hi > n_chunks) c_hi = n_chunks;
+        for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
+        ol[k] = 0;
+        kv[k] = -1;
+        if (u < n_utt) {
+            const uint64_t len = o[k + 2] - o[k + 1];
+            ol[k] = (uint32_t)len;
+            kv[k] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
+            if (wc_n) wc_n[u] = 0;
+            // a row that some slice boundary cuts (same test as g_cut)
+            if (long_min != NO_CUTS && len > long_min) {
+                const uint64_t kk = ((o[k + 1] - base + r0) >> lane_shift) + 1;      // first boundary after its start
+                if (kk < n_chunks && ((int64_t)(kk << lane_shift) - (int64_t)r0) < (int64_t)(o[k + 2] - base))
+                    long_rows[atomicAdd(long_count, 1u)] = u;
+            }
+        }
+    }
+    // row defaults (no findings: out_len = len; keyword group = the always-present group for AGENT
+    // rows, else -1): 16-byte stores for a full group (the arrays are the engine's, 16-byte aligned)
+    if (u0 + CI_ROWS <= n_utt) {
+        *reinterpret_cast<uint4*>(out_len + u0) = make_uint4(ol[0], ol[1], ol[2], ol[3]);
+        *reinterpret_cast<int4*>(kw + u0) = make_int4(kv[0], kv[1], kv[2], kv[3]);
+    } else {
+        for (int k = 0; k < CI_ROWS && u0 + k < n_utt; ++k) {
+            out_len[u0 + k] = ol[k];
+            kw[u0 + k] = kv[k];
         }
     }
 }
@@ -3936,7 +3966,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));       // err, long_count, ncommit, pair_count
     HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
-        k_chunk_index<<<(n_utt + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
+        k_chunk_index<<<(n_utt / CI_ROWS + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
                                                                 e->long_min, R.kw_always_min, e->first_utt,
                                                                 e->out_len, e->kw, win_ctx ? e->wc_n : nullptr,
                                                                 e->long_rows, e->long_count, base, total_bytes, e->d_err);
