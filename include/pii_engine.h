@@ -132,7 +132,9 @@ int pii_context_get(struct pii_engine* e, uint32_t slot, int32_t* group, int64_t
 int pii_context_set(struct pii_engine* e, uint32_t slot, int32_t group, int64_t ts_us);
 
 /* per-info-type counts of kept findings since the last reset (counts[n_types]); the multi-GPU
- * driver all-reduces these over RCCL */
+ * driver all-reduces these over RCCL.  Each call copies the counts to pinned host memory with its
+ * totals, so reading them after pii_sync costs no further device round trip.  The reset is
+ * stream-ordered (no host wait): the next call starts from zero, on any stream. */
 int pii_histogram(struct pii_engine* e, uint64_t* counts, uint32_t n);
 int pii_histogram_reset(struct pii_engine* e);
 
