@@ -759,9 +759,11 @@ def window_main(args):
 
     def step(k):
         o = offs.data_ptr() + 8 * k * C
-        eng.rescan_window_device(text.data_ptr(), o, C, slot.data_ptr() + 4 * k * C, role.data_ptr() + k * C,
-                                 ts.data_ptr() + 8 * k * C, d_out.data_ptr(), out_cap, d_oo.data_ptr(),
-                                 d_sp.data_ptr(), span_cap, d_ctx.data_ptr())
+        # the step's rows are resident and their span known: no device-to-host read before the launch
+        eng.rescan_window_device_ex(text.data_ptr(), o, C, int(meta.offsets[k * C]), step_bytes[k],
+                                    slot.data_ptr() + 4 * k * C, role.data_ptr() + k * C, ts.data_ptr() + 8 * k * C,
+                                    d_out.data_ptr(), out_cap, d_oo.data_ptr(), d_sp.data_ptr(), span_cap,
+                                    d_ctx.data_ptr())
         ob, ns, fl = eng.sync()
         if fl:
             raise RuntimeError(f"engine error flags {fl}")

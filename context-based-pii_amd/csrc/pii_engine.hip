@@ -4989,6 +4989,16 @@ int pii_rescan_window_device(pii_engine* e, const uint8_t* d_bytes, const uint64
                        d_out_offsets, d_spans, span_cap, d_win_ctx, stream, nullptr);
 }
 
+int pii_rescan_window_device_ex(pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                                uint64_t batch_base, uint64_t batch_bytes, const uint32_t* d_conv_slot,
+                                const uint8_t* d_role, const int64_t* d_ts_us, uint8_t* d_out_bytes, uint64_t out_cap,
+                                uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_win_ctx,
+                                void* stream) {
+    const uint64_t decl[2] = {batch_base, batch_bytes};
+    return device_call(e, true, d_bytes, d_offsets, n_utt, d_conv_slot, d_role, d_ts_us, d_out_bytes, out_cap,
+                       d_out_offsets, d_spans, span_cap, d_win_ctx, stream, decl);
+}
+
 int pii_context_get(pii_engine* e, uint32_t slot, int32_t* group, int64_t* ts_us) {
     if (!e || slot >= e->n_slots) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));

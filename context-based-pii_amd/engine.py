@@ -25,7 +25,8 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_reserve", "pii_sync", "pii_context_get",
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
-           "pii_window_count", "pii_rescan_window", "pii_rescan_window_device"]
+           "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
+           "pii_rescan_window_device_ex"]
 
 
 class PiiError(RuntimeError):
@@ -97,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_window_count.argtypes = [P, c.c_uint32, U32]
     lib.pii_rescan_window.argtypes = lib.pii_scan_redact.argtypes
     lib.pii_rescan_window_device.argtypes = lib.pii_scan_redact_device.argtypes
+    lib.pii_rescan_window_device_ex.argtypes = lib.pii_scan_redact_device_ex.argtypes
     for name in EXPORTS:
         if name != "pii_last_error":
             getattr(lib, name).restype = c.c_int
@@ -212,6 +214,16 @@ class Engine:
                                                out_cap, d_out_offsets, d_spans, span_cap, d_ctx, stream)
         if rc != PII_OK:
             raise self._err(rc, "pii_rescan_window_device")
+
+    def rescan_window_device_ex(self, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot, d_role, d_ts,
+                                d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx=None, stream=None) -> None:
+        """rescan_window_device with offsets[0] and the batch size stated by the caller (no device-to-host
+        read before the launch; pii_rescan_window_device_ex)"""
+        rc = self.lib.pii_rescan_window_device_ex(self.h, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot,
+                                                  d_role, d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap,
+                                                  d_ctx, stream)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_rescan_window_device_ex")
 
     def _host_call(self, fn, name, texts, conv_slot, role, ts_us, mult) -> BatchResult:
         data, offs = pack(texts)

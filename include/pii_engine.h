@@ -188,6 +188,13 @@ int pii_rescan_window_device(struct pii_engine* e, const uint8_t* d_bytes, const
                              const int64_t* d_ts_us, uint8_t* d_out_bytes, uint64_t out_cap,
                              uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap,
                              int16_t* d_win_ctx, void* stream);
+/* The same with offsets[0] and the byte size stated by the caller (as pii_scan_redact_device_ex):
+ * a re-scan step enqueues without any device-to-host read. */
+int pii_rescan_window_device_ex(struct pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                                uint32_t n_utt, uint64_t batch_base, uint64_t batch_bytes,
+                                const uint32_t* d_conv_slot, const uint8_t* d_role, const int64_t* d_ts_us,
+                                uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets,
+                                pii_span* d_spans, uint32_t span_cap, int16_t* d_win_ctx, void* stream);
 
 #ifdef __cplusplus
 }
