@@ -1167,8 +1167,9 @@ constexpr int PAIRS_BLOCK = 256;
 // front, group 0 (built-ins and excluders) comes first among one start's pairs.  Only group 0 steps
 // the keyword automaton.  The count pass also writes each lane's total event count (lane_evn).
 constexpr int SCAN_GROUPS_MAX = 8;
-struct AccTabs {                 // per SCAN group: transition index -> global D accept-set id
-    const uint16_t* accid[SCAN_GROUPS_MAX];
+struct AccTabs {                 // per SCAN group, by D transition index:
+    const uint16_t* accid[SCAN_GROUPS_MAX];   // global D accept-set id
+    const uint16_t* npair[SCAN_GROUPS_MAX];   // pairs of that accept set
 };
 
 template <bool WRITE, bool MULTI>
@@ -1386,7 +1387,9 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
                                                     const uint64_t* __restrict__ lane_pair,
                                                     const uint64_t* __restrict__ lane_ev,
                                                     uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err,
-                                                    PairRes* __restrict__ pres) {
+                                                    PairRes* __restrict__ pres, const AccTabs acct,
+                                                    uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
+                                                    uint32_t* __restrict__ lane_evn) {
     __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
     __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
     __shared__ uint32_t s_aoff[257];
@@ -1420,6 +1423,18 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
     if (cw0 >= n_chunks) return;
     auto uoff = [&](uint32_t u) { return staged ? so[u - U0] : (uint32_t)((int64_t)offs[u] - base); };
     const bool valid = c < n_chunks;
+    // count pass over several SCAN groups (config 5): blockIdx.y = group, its own event arena and
+    // per-transition pair counts; only group 0 carries the keyword automaton.  The lanes' pair counts
+    // add up over the groups (lane_np is zeroed first), group 0 writes the lanes' total event counts.
+    const uint32_t q = WRITE ? 0u : blockIdx.y;
+    const uint16_t* __restrict__ npair = q ? acct.npair[q] : R.d_npair;
+    if (!WRITE && n_groups > 1 && q == 0 && valid) {
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < n_groups; ++k) tot += lane_cnt[(uint64_t)k * cnt_stride + c];
+        lane_evn[c] = tot;
+    }
+    ev += (uint64_t)q * ev_stride;
+    lane_cnt += (uint64_t)q * cnt_stride;
     const uint32_t cnt = valid ? lane_cnt[c] : 0u;
     uint32_t eb = 0, u0 = 0, u1 = 0;                      // the lane's arena, utterances [u0, u1)
     if (cnt) {
@@ -1462,7 +1477,7 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
         uint32_t n = 0, acc = 0, u = 0;
         if (act) {
             E = ev[(uint64_t)o_eb + (f - o_ex)];
-            n = R.d_npair[E.sd];
+            n = npair[E.sd];
             if (WRITE) acc = R.d_accid[E.sd];
             uint32_t lo = o_u0, hi = o_u1 - 1;            // last u with start <= pos
             while (lo < hi) {
@@ -1490,7 +1505,7 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
                     Lc.uend = uoff(u + 1);
                     evloc[E0 + f] = Lc;
                 }
-            } else {
+            } else if (q == 0) {
                 const uint32_t kg = R.k_grp[E.sk];
                 if (kg != (uint32_t)KW_NONE && (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT)
                     atomicMin(reinterpret_cast<unsigned int*>(kw + u), kg);
@@ -1537,7 +1552,10 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
         const uint32_t add = __shfl(sc, last);
         if (here) run += add;
     }
-    if (!WRITE && valid) lane_np[c] = run;
+    if (!WRITE && valid) {
+        if (n_groups > 1) atomicAdd(lane_np + c, run);
+        else lane_np[c] = run;
+    }
 }
 
 // one thread per event: its (start, pattern) pairs, accept-set order (excluders first)
@@ -3998,15 +4016,11 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             const bool multi = e->n_sg > 1;
             const uint32_t ns = e->n_sg, cs = (uint32_t)e->cap_lanes;
             const uint64_t es = e->cap_ev;
-            if (multi)
-                k_pairs<false, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
-                                                                  e->lane_evn);
-            else
-                k_pairs_flat<false><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                 e->lane_ev, e->lane_np, e->d_err, e->pres);
+            if (multi) HIPCHK(hipMemsetAsync(e->lane_np, 0, (size_t)n_chunks * sizeof(uint32_t), st));
+            k_pairs_flat<false><<<dim3(nbp, ns), PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
+                                                                       e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                       e->lane_ev, e->lane_np, e->d_err, e->pres, e->acct,
+                                                                       ns, es, cs, e->lane_evn);
             int rc;
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st, multi ? e->lane_evn : e->lane_cnt,
                                      n_chunks, e->lane_ev)))
@@ -4020,7 +4034,8 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             } else {
                 k_pairs_flat<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                e->lane_ev, e->lane_np, e->d_err, e->pres);
+                                                                e->lane_ev, e->lane_np, e->d_err, e->pres, e->acct,
+                                                                1, 0, 0, nullptr);
             }
         }
         HIPCHK(hipGetLastError());
@@ -4395,7 +4410,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     struct HostGroup {
         int SD, CD, CDs, start;
         uint32_t lds;
-        std::vector<uint16_t> td, tk, dacc, kacc;
+        std::vector<uint16_t> td, tk, dacc, kacc, npair;
         std::vector<uint32_t> cmap4;
     };
     std::vector<HostGroup> hg;
@@ -4454,6 +4469,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         const uint32_t* off = reinterpret_cast<const uint32_t*>(find("scan.d.acc_off")->data);
         for (size_t i = 0; i < dacc.size(); ++i) d_npair[i] = (uint16_t)(off[dacc[i] + 1] - off[dacc[i]]);
         for (size_t i = 0; i < kacc.size(); ++i) k_grp[i] = kacc[i] ? k_acc_min[kacc[i]] : (uint16_t)KW_NONE;
+        for (auto& h : hg) {
+            h.npair.resize(h.dacc.size());
+            for (size_t i = 0; i < h.dacc.size(); ++i) h.npair[i] = (uint16_t)(off[h.dacc[i] + 1] - off[h.dacc[i]]);
+        }
     }
     size_t i_dnp = add(d_npair.data(), d_npair.size() * 2), i_kgrp = add(k_grp.data(), k_grp.size() * 2);
     size_t i_dt = addsec("det.type"), i_dv = addsec("det.validator"), i_dl = addsec("det.lik"),
@@ -4462,11 +4481,12 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
            i_ro = addsec("var.rule_off"), i_ri = addsec("var.rule_ids"), i_eo = addsec("var.excl_off"),
            i_ei = addsec("var.excl_ids"), i_to = add(tok_off.data(), tok_off.size() * 4),
            i_tb = add(tok.data(), tok.size());
-    struct GroupPut { size_t cmap, td, tk, dacc, kacc; };
+    struct GroupPut { size_t cmap, td, tk, dacc, kacc, npair; };
     std::vector<GroupPut> gp;
     for (auto& h : hg)
         gp.push_back({add(h.cmap4.data(), 1024), add(h.td.data(), h.td.size() * 2), add(h.tk.data(), 4),
-                      add(h.dacc.data(), h.dacc.size() * 2), add(h.kacc.data(), 4)});
+                      add(h.dacc.data(), h.dacc.size() * 2), add(h.kacc.data(), 4),
+                      add(h.npair.data(), h.npair.size() * 2)});
     if (hipSetDevice(device) != hipSuccess) { e->err = "hipSetDevice failed"; pii_engine_destroy(e); return PII_E_DEVICE; }
     if (hipMalloc(&e->d_rules, total) != hipSuccess) return fail("hipMalloc rules failed");
     std::vector<uint8_t> host(total, 0);
@@ -4587,6 +4607,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     e->sg.assign(1, R);
     e->sg_lds.assign(1, e->scan_lds);
     e->acct.accid[0] = R.d_accid;
+    e->acct.npair[0] = R.d_npair;
     for (size_t q = 0; q < hg.size(); ++q) {
         RulesDev Rq = R;
         const HostGroup& h = hg[q];
@@ -4595,6 +4616,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         Rq.tk = (const uint16_t*)at(gp[q].tk);
         Rq.d_accid = (const uint16_t*)at(gp[q].dacc);
         Rq.k_accid = (const uint16_t*)at(gp[q].kacc);
+        Rq.d_npair = (const uint16_t*)at(gp[q].npair);
         Rq.SD = h.SD;
         Rq.CD = h.CD;
         Rq.CDs = h.CDs;
@@ -4606,6 +4628,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->sg.push_back(Rq);
         e->sg_lds.push_back(h.lds);
         e->acct.accid[q + 1] = Rq.d_accid;
+        e->acct.npair[q + 1] = Rq.d_npair;
     }
     const size_t max_lds = *std::max_element(e->sg_lds.begin(), e->sg_lds.end());
     if (max_lds > 64 * 1024 &&

@@ -1,0 +1,68 @@
+"""A/B timing of ner_gemm builds (BERT-base shapes, 64 x 128 tokens) beside torch.nn.functional.linear
+(hipBLASLt), with a numerics check of every build against torch.  usage: python tools/gemm_ab.py LIB..."""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "context-based-pii_amd"))
+import ner  # noqa: E402
+
+SHAPES = [("qkv", 8192, 2304, 768, 0), ("out", 8192, 768, 768, 2), ("ffn1", 8192, 3072, 768, 1),
+          ("ffn2", 8192, 768, 3072, 2)]
+
+
+def timeit(fn, reps=50):
+    for _ in range(5):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3     # us
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    res = {}
+    for name, M, N, K, epi in SHAPES:
+        A = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
+        W = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+        b = torch.randn(N, generator=g).to(dev)
+        R = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        ref = torch.nn.functional.linear(A.float(), W.float(), b)
+        if epi == 1:
+            ref = torch.nn.functional.gelu(ref)
+        elif epi == 2:
+            ref = ref + R.float()
+        flop = 2.0 * M * N * K
+        row = {"torch_linear_us": timeit(lambda: torch.nn.functional.linear(A, W, b.to(torch.bfloat16)))}
+        for path in sys.argv[1:]:
+            lib = ner.load_library(os.path.join(ROOT, path))
+            st = torch.cuda.current_stream().cuda_stream
+
+            def run():
+                rc = lib.ner_gemm(A.data_ptr(), W.data_ptr(), b.data_ptr(), R.data_ptr(), C.data_ptr(), M, N, K, epi,
+                                  st)
+                assert rc == 0
+            run()
+            torch.cuda.synchronize()
+            err = ((C.float() - ref).norm() / ref.norm()).item()
+            us = timeit(run)
+            row[os.path.basename(path)] = {"us": round(us, 1), "tflops": round(flop / us / 1e6, 1),
+                                           "rel_l2": round(err, 5)}
+        row["torch_tflops"] = round(flop / row["torch_linear_us"] / 1e6, 1)
+        res[name] = row
+        print(name, json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
