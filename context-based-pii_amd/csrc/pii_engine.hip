@@ -1157,15 +1157,17 @@ static_assert(sizeof(SelRec) == sizeof(FirstCont), "SelRec aliases the FirstCont
 // PAIRS_UCAP utterances (very short rows) walks global memory instead.
 constexpr int PAIRS_BLOCK = 256;
 
-// Two launches: WRITE = false counts each lane's pairs (and records the AGENT rows' keyword groups),
-// an exclusive scan of the counts gives every lane its block of the queue (lane order, no atomics),
-// WRITE = true fills the blocks.
+// Two passes: k_pairs_flat<false> counts each lane's pairs (and records the AGENT rows' keyword
+// groups), an exclusive scan of the counts gives every lane its block of the queue (lane order, no
+// atomics), the write pass fills the blocks.
 //
 // MULTI (a rule set split over several SCAN groups, config 5): every group's k_scan pass wrote its
-// own per-lane event list (descending position, arena g at ev + g * ev_stride); the lists are merged
-// here by position, a tie going to the higher group first so that, the queue being filled back to
-// front, group 0 (built-ins and excluders) comes first among one start's pairs.  Only group 0 steps
-// the keyword automaton.  The count pass also writes each lane's total event count (lane_evn).
+// own per-lane event list (descending position, arena g at ev + g * ev_stride), counted per group by
+// the flat pass.  The write pass here merges the lists by position, a tie going to the higher group
+// first so that, the queue being filled back to front, group 0 (built-ins and excluders) comes first
+// among one start's pairs; k_expand then writes the pairs.  (Measured alternative: this walk
+// assigning only each event's first pair index, the records then written by the flat pass per
+// group -- 2.30 + 1.61 ms against 3.19 + 0.39 ms here; the merge walk itself is the cost.)
 constexpr int SCAN_GROUPS_MAX = 8;
 struct AccTabs {                 // per SCAN group, by D transition index:
     const uint16_t* accid[SCAN_GROUPS_MAX];   // global D accept-set id
@@ -1184,9 +1186,7 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
                                                uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
                                                const AccTabs acct, uint32_t* __restrict__ lane_evn) {
     __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
-    __shared__ uint8_t s_role[PAIRS_BLOCK / 64][PAIRS_UCAP];
     __shared__ uint32_t s_acc_off[256];
-    __shared__ uint16_t s_kmin[256];
     if (*err & ERR_ARGS) return;
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1195,9 +1195,8 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     const uint64_t* __restrict__ offs = g.offs;
     const int64_t base = (int64_t)g.base;
     // small accept-set tables (<= 256 sets; larger rule sets read them from global memory)
-    const uint32_t n_dacc = R.n_dacc, n_kacc = R.n_kacc;
+    const uint32_t n_dacc = R.n_dacc;
     for (uint32_t i = threadIdx.x; i <= n_dacc && i < 256; i += PAIRS_BLOCK) s_acc_off[i] = R.d_acc_off[i];
-    for (uint32_t i = threadIdx.x; i < n_kacc && i < 256; i += PAIRS_BLOCK) s_kmin[i] = R.k_acc_min[i];
     // the wavefront's utterances [U0, U1] (from one before its first lane's first start: a cut row)
     const uint32_t cw0 = c - lane;
     const uint32_t cw1 = min(cw0 + 64, n_chunks);
@@ -1205,17 +1204,12 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     const uint32_t U1 = cw0 < n_chunks ? g.first_utt[cw1] : 0u;
     const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
     uint32_t* so = s_off[wv];
-    uint8_t* sr = s_role[wv];
-    if (staged && cw0 < n_chunks) {
+    if (staged && cw0 < n_chunks)
         for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)((int64_t)offs[U0 + k] - base);
-        for (uint32_t k = lane; k < U1 - U0; k += 64) sr[k] = role[U0 + k];
-    }
     __syncthreads();
-    const bool small_acc = n_dacc < 256 && n_kacc <= 256;
+    const bool small_acc = n_dacc < 256;
     auto acc_off = [&](uint32_t a) { return small_acc ? s_acc_off[a] : R.d_acc_off[a]; };
-    auto kmin = [&](uint32_t a) { return small_acc ? (uint32_t)s_kmin[a] : (uint32_t)R.k_acc_min[a]; };
     auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : (int64_t)offs[u] - base; };
-    auto uagent = [&](int64_t u) { return (staged ? sr[u - U0] : role[u]) == PII_ROLE_AGENT; };
 
     // the lane's events in descending position: one list, or the merge of the groups' lists
     uint32_t cnt = 0;
@@ -1276,57 +1270,7 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
         k0 = best == 0;
     };
 
-    if (!WRITE) {
-        // count pairs, keyword groups of AGENT rows (a cut row's lanes merge theirs with an atomic min:
-        // -1 = no hit is the largest unsigned value)
-        auto put_kw = [&](int64_t u, int grp) {
-            const int v = min(grp, R.kw_always_min);
-            if ((L.clo && u == (int64_t)L.u0) || (L.chi && u == u_top))
-                atomicMin(reinterpret_cast<unsigned int*>(kw + u), (unsigned int)v);
-            else
-                kw[u] = v;
-        };
-        uint32_t np = 0;
-        int64_t u = u_top;
-        int64_t s_u = cnt ? uoff(u) : 0;
-        bool agent = cnt ? uagent(u) : false;
-        int grp = KW_NONE;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            Event E;
-            uint32_t acc = 0;
-            bool k0 = true;
-            if (MULTI) {
-                next(E, acc, k0);
-            } else {                        // one list: per-transition pair counts / keyword groups
-                E = En;
-                if (k + 1 < cnt) En = evl[k + 1];
-            }
-            const int64_t pos = E.pos;
-            while (pos < s_u) {
-                if (grp != KW_NONE) put_kw(u, grp);
-                grp = KW_NONE;
-                --u;
-                s_u = uoff(u);
-                agent = uagent(u);
-            }
-            if (MULTI) {
-                np += acc_off(acc + 1) - acc_off(acc);
-                if (agent && k0) {
-                    const uint32_t a = R.k_accid[E.sk];
-                    if (a) grp = min(grp, (int)kmin(a));
-                }
-            } else {
-                np += R.d_npair[E.sd];
-                if (agent) grp = min(grp, (int)R.k_grp[E.sk]);
-            }
-        }
-        if (cnt && grp != KW_NONE) put_kw(u, grp);
-        if (valid) {
-            lane_np[c] = np;
-            if (MULTI) lane_evn[c] = cnt;
-        }
-        return;
-    }
+    static_assert(WRITE && MULTI, "counting is k_pairs_flat<false>, one SCAN group k_pairs_flat<true>");
     if (!valid) return;
     const uint32_t np = lane_np[c];
     const uint64_t my = lane_pair[c];
