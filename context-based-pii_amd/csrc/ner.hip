@@ -46,13 +46,15 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // 2 x 2 MFMAs on its 64 x 64 quarter.  LDS rows are 128 B with the 16-byte chunks XOR-swizzled by
 // (row & 7) -- chunk c of row r is stored at position c ^ (r & 7) -- so the fragment reads of 8
 // consecutive rows (one ds_read_b128 lane group) hit 8 different 16-byte bank groups; the swizzle is
-// applied on the per-lane GLOBAL address, since an LDS-DMA writes lane l at base + 16 l.  Two LDS
-// buffers (2 x 32 KiB) and one barrier per step: slab k + 1 is in flight while slab k is multiplied.
+// applied on the per-lane GLOBAL address, since an LDS-DMA writes lane l at base + 16 l.  One LDS
+// buffer (32 KiB) and two barriers per step: latency is hidden by 3-4 workgroups per CU.
 template <int EPI>
 __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
                                                     const float* __restrict__ bias, const uint16_t* __restrict__ R,
                                                     uint16_t* __restrict__ C, int M, int N, int K) {
-    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (GB_M + GB_N) * GB_K];
+    __shared__ __attribute__((aligned(16))) uint16_t smem[(GB_M + GB_N) * GB_K];
+    uint16_t* sA = smem;
+    uint16_t* sB = smem + GB_M * GB_K;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // XCD-aware tile order (bijective): workgroups are dealt to the 8 XCDs round robin, so give each
     // XCD a contiguous run of tile ids -- the N tiles of one M row-block share their A rows in its L2
@@ -78,25 +80,14 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
     const int r = lane & 31, h = lane >> 5;
-    // slab k0 -> LDS buffer b (two buffers: the DMA of slab k + 1 runs under the MFMAs of slab k)
-    auto fetch = [&](int k0, int b) {
-        uint16_t* dA = smem + b * (GB_M + GB_N) * GB_K;
-        uint16_t* dB = dA + GB_M * GB_K;
+    for (int k0 = 0; k0 < K; k0 += GB_K) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int blk = (i * 4 + wave) * 64 * 8;      // this wave-instruction's 1 KiB of LDS
-            __builtin_amdgcn_global_load_lds((gptr_t)(srcA[i] + k0), (lptr_t)(dA + blk), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gptr_t)(srcB[i] + k0), (lptr_t)(dB + blk), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcA[i] + k0), (lptr_t)(sA + blk), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcB[i] + k0), (lptr_t)(sB + blk), 16, 0, 0);
         }
-    };
-    fetch(0, 0);
-    for (int k0 = 0, b = 0; k0 < K; k0 += GB_K, b ^= 1) {
-        // slab k0 has landed (each wave waits for its DMAs; the barrier publishes them) and every wave
-        // is done with the other buffer, which the next slab's DMA now overwrites
         __syncthreads();
-        if (k0 + GB_K < K) fetch(k0 + GB_K, b ^ 1);
-        const uint16_t* sA = smem + b * (GB_M + GB_N) * GB_K;
-        const uint16_t* sB = sA + GB_M * GB_K;
 #pragma unroll
         for (int ks = 0; ks < GB_K / 16; ++ks) {
             bf16x8 fa[2], fb[2];
@@ -113,9 +104,9 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
+        __syncthreads();
     }
-    __syncthreads();
-    // epilogue through LDS (the K loop left it free), 64 rows at a time: the two wavefronts
+    // epilogue through LDS (the K loop left it free: 32 KiB), 64 rows at a time: the two wavefronts
     // holding those rows store their accumulators as a row-major f32 [64][128] image (C/D map of
     // 32x32x16: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)); then every thread
     // finishes 8-column chunks with 16-byte loads of the residual and 16-byte stores of C
