@@ -1231,14 +1231,19 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
     const Event* evl = ev + evoff;
     uint32_t k1 = 0;                        // single list: next index
     Event En = (!MULTI && cnt) ? evl[0] : Event{};
-    uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX];
-    Event gh[SCAN_GROUPS_MAX];
+    // the groups' list heads in registers (position, sd | sk << 16); the merge step is branch-free:
+    // the winning group's head, table and next event are picked with select trees, so every step
+    // issues one accept-set load and one event load for the whole wavefront (a per-group branch
+    // would issue them once per group, each with a few lanes active)
+    uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX], hp[SCAN_GROUPS_MAX], hx[SCAN_GROUPS_MAX];
     if (MULTI) {
 #pragma unroll
         for (int q = 0; q < SCAN_GROUPS_MAX; ++q) {
             gk[q] = 0;
             gn[q] = (cnt && (uint32_t)q < n_groups) ? lane_cnt[(uint64_t)q * cnt_stride + c] : 0u;
-            gh[q] = gn[q] ? evl[(uint64_t)q * ev_stride] : Event{};
+            const Event H = gn[q] ? evl[(uint64_t)q * ev_stride] : Event{};
+            hp[q] = H.pos;
+            hx[q] = (uint32_t)H.sd | (uint32_t)H.sk << 16;
         }
     }
     // next event (E) and its D accept set; k0: it is group 0's (the keyword automaton's group)
@@ -1251,21 +1256,41 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
             k0 = true;
             return;
         }
-        int best = -1;
-        uint32_t bp = 0;
+        uint32_t best = 0, bp = 0;
+        bool any = false;
 #pragma unroll
         for (int q = SCAN_GROUPS_MAX - 1; q >= 0; --q)
-            if (gk[q] < gn[q] && (best < 0 || gh[q].pos > bp)) {
-                best = q;
-                bp = gh[q].pos;
+            if (gk[q] < gn[q] && (!any || hp[q] > bp)) {
+                best = (uint32_t)q;
+                bp = hp[q];
+                any = true;
             }
+        uint32_t x = 0, kb = 0, nb = 0;
 #pragma unroll
         for (int q = 0; q < SCAN_GROUPS_MAX; ++q)
-            if (q == best) {
-                E = gh[q];
-                acc = acct.accid[q][E.sd];
-                ++gk[q];
-                if (gk[q] < gn[q]) gh[q] = evl[(uint64_t)q * ev_stride + gk[q]];
+            if ((uint32_t)q == best) {
+                x = hx[q];
+                kb = gk[q] + 1u;
+                nb = gn[q];
+            }
+        E.pos = bp;
+        E.sd = (uint16_t)(x & 0xffffu);
+        E.sk = (uint16_t)(x >> 16);
+        const bool b0 = best & 1u, b1 = best & 2u, b2 = best & 4u;
+        const uint16_t* t01 = b0 ? acct.accid[1] : acct.accid[0];
+        const uint16_t* t23 = b0 ? acct.accid[3] : acct.accid[2];
+        const uint16_t* t45 = b0 ? acct.accid[5] : acct.accid[4];
+        const uint16_t* t67 = b0 ? acct.accid[7] : acct.accid[6];
+        const uint16_t* tab = b2 ? (b1 ? t67 : t45) : (b1 ? t23 : t01);
+        acc = tab[E.sd];
+        Event H{};
+        if (kb < nb) H = evl[(uint64_t)best * ev_stride + kb];
+#pragma unroll
+        for (int q = 0; q < SCAN_GROUPS_MAX; ++q)
+            if ((uint32_t)q == best) {           // register updates only (selects)
+                gk[q] = kb;
+                hp[q] = H.pos;
+                hx[q] = (uint32_t)H.sd | (uint32_t)H.sk << 16;
             }
         k0 = best == 0;
     };
