@@ -548,11 +548,11 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, 
 #define SCAN_STEP8(J, H)                                                                          \
     {                                                                                             \
         ad[J] = (nd & ~pm & 0xfffcu) + (cc[J] & 0xffffu);                                         \
-        ak[J] = (nk & ~pm & 0xfffcu) + (cc[J] >> 16);                                             \
+        ak[J] = HK ? (nk & ~pm & 0xfffcu) + (cc[J] >> 16) : tk_base;                              \
         nd = lds_u16(ad[J]);                                                                      \
-        nk = lds_u16(ak[J]);                                                                      \
+        if (HK) nk = lds_u16(ak[J]);                                                              \
         asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(pm) : "v"(b16), "n"((H) + (J)));                   \
-        m = __builtin_amdgcn_alignbit(nd | nk, m, 2);                                             \
+        m = __builtin_amdgcn_alignbit(HK ? nd | nk : nd, m, 2);                                   \
     }
 
 #define SCAN_GROUP8(W, H, OFF)                                                                    \
@@ -584,7 +584,10 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
     e_len = e_hi - e_lo;                 // wraps for an empty range: nothing is emitted
 }
 
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+// HK = false: a SCAN group >= 1, whose K is the never-accepting one-row stub -- K is not stepped (its
+// row stays the start row, its transition is the stub's class-0 entry), one LDS read less per byte
+template <bool HK>
+__global__ __launch_bounds__(SCAN_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
@@ -3974,7 +3977,8 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(Rq, g, text, e->lane_pos,
                                                                      q == 0 ? e->bnd : nullptr, stq);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
-                k_scan<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK, e->sg_lds[q], st>>>(
+                (q == 0 ? k_scan<true> : k_scan<false>)<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK,
+                                                            e->sg_lds[q], st>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
                 if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
                 if (e->long_min != NO_CUTS)
@@ -4601,7 +4605,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     }
     const size_t max_lds = *std::max_element(e->sg_lds.begin(), e->sg_lds.end());
     if (max_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) != hipSuccess)
+        (hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
+             hipSuccess))
         return fail("cannot raise LDS limit");
     if (max_lds + FIX_LDS > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize,
