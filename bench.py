@@ -122,7 +122,8 @@ def measured_traffic(kernel: str, n_bytes: int):
         t = json.load(open(path))
     except (OSError, ValueError):
         return None
-    k = t.get("kernels", {}).get(kernel)
+    ks = t.get("kernels", {})
+    k = ks.get(kernel) or ks.get(kernel + "<true>")       # (k_scan is a template: k_scan<true> = SCAN group 0)
     if not k or t.get("source_digest") != source_digest() or t.get("bytes_per_gpu") != n_bytes:
         return None
     return k.get("hbm_bytes")
