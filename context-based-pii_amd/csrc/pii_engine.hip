@@ -2585,6 +2585,10 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
 // start) order) and the RSpan list; per-workgroup per-type histogram partials.  A finding's output
 // position = its utterance's output offset + its start + the deltas of the utterance's earlier
 // findings (for a cut row, starting from lane_rowbase: the row's findings in earlier lanes).
+// Wave-cooperative (as k_pairs_flat): the 64 lanes' findings are one flattened list, 64 at a time --
+// finding f belongs to the first lane whose inclusive count exceeds f, the running delta is a
+// segmented scan over (lane, utterance) runs plus each lane's carry from the previous 64, and one
+// store instruction writes 64 neighbouring records (the per-lane walk wrote record k of 64 lanes).
 __global__ __launch_bounds__(256) void k_spans(const RulesDev R, const Geo g, const pii_span* __restrict__ fd,
                                                const uint32_t* __restrict__ lane_nf,
                                                const uint64_t* __restrict__ lane_sp,
@@ -2594,34 +2598,83 @@ __global__ __launch_bounds__(256) void k_spans(const RulesDev R, const Geo g, co
                                                uint32_t* __restrict__ hist_part, uint32_t hist_types) {
     __shared__ uint32_t sh_hist[1024];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const bool run = *err == 0;
     for (uint32_t i = threadIdx.x; i < hist_types; i += blockDim.x) sh_hist[i] = 0;
     __syncthreads();
     const uint32_t nf = run && c < g.n_chunks ? lane_nf[c] : 0u;
+    uint64_t fb = 0, sp0 = 0;            // the lane's findings arena, its first span index
+    uint32_t cu0 = 0xffffffffu;          // a lane cut at lo: the cut row (its running delta starts at rb)
+    int32_t rb = 0;
     if (nf) {
         const Lane L = g_lane(g, c);
-        const pii_span* f0 = fd + fd_base(L, c, R.min_len);
-        const uint64_t sp0 = lane_sp[c];
-        uint32_t u = 0xffffffffu;
-        int64_t running = 0, ubase_in = 0, ubase_out = 0;
-        for (uint32_t k = 0; k < nf; ++k) {
-            const pii_span F = f0[k];
-            if (F.utt != u) {
-                u = F.utt;
-                running = (L.clo && u == L.u0) ? lane_rowbase[c] : 0;
-                ubase_in = g_off(g, u);
-                ubase_out = (int64_t)out_offs[u];
-            }
-            spans[sp0 + k] = F;
-            const uint32_t t = F.info_type;
-            const int64_t tl = (int64_t)(R.tok_off[t + 1] - R.tok_off[t]);
+        fb = fd_base(L, c, R.min_len);
+        sp0 = lane_sp[c];
+        if (L.clo) {
+            cu0 = L.u0;
+            rb = lane_rowbase[c];
+        }
+    }
+    uint32_t incl = nf;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 63), excl = incl - nf;
+    uint32_t carry_u = 0xffffffffu;      // lane: utterance of its last finding handled, running delta after it
+    int64_t carry_run = 0;
+    for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+        const uint32_t f = f0 + lane;
+        const bool act = f < total;
+        int ow = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            const uint32_t v = __shfl(incl, ow + step - 1);
+            if (v <= f) ow += step;
+        }
+        const uint32_t o_ex = __shfl(excl, ow), o_cu0 = __shfl(cu0, ow), o_cu = __shfl(carry_u, ow);
+        const int32_t o_rb = __shfl(rb, ow);
+        const int64_t o_crun = __shfl(carry_run, ow);
+        const uint64_t o_fb = __shfl(fb, ow), o_sp = __shfl(sp0, ow);
+        const uint32_t k = f - o_ex;
+        pii_span F{};
+        int64_t d = 0;
+        uint32_t t = 0;
+        if (act) {
+            F = fd[o_fb + k];
+            t = F.info_type;
+            d = (int64_t)(R.tok_off[t + 1] - R.tok_off[t]) - (int64_t)(F.end - F.start);
+        }
+        const uint32_t uk = act ? F.utt : 0xffffffffu;
+        // running delta before this finding: its (lane, utterance) run's base + the run's earlier deltas
+        int64_t sc = d;
+#pragma unroll
+        for (int dl = 1; dl < 64; dl <<= 1) {
+            const int64_t o = __shfl_up(sc, dl);
+            const int oo = __shfl_up(ow, dl);
+            const uint32_t ou = __shfl_up(uk, dl);
+            if (lane >= dl && oo == ow && ou == uk) sc += o;
+        }
+        const int64_t base = uk == o_cu ? o_crun : (uk == o_cu0 ? (int64_t)o_rb : 0);
+        if (act) {
+            spans[o_sp + k] = F;
+            const int64_t ubase_in = g_off(g, F.utt), ubase_out = (int64_t)out_offs[F.utt];
             RSpan rs;
             rs.in_lo = (uint32_t)(ubase_in + F.start);
             rs.in_hi = (uint32_t)(ubase_in + F.end);
-            rs.out = (uint64_t)(ubase_out + F.start + running) | ((uint64_t)t << 48);
-            rsp[sp0 + k] = rs;
-            running += tl - (int64_t)(F.end - F.start);
+            rs.out = (uint64_t)(ubase_out + F.start + base + (sc - d)) | ((uint64_t)t << 48);
+            rsp[o_sp + k] = rs;
             if (t < hist_types) atomicAdd(&sh_hist[t], 1u);
+        }
+        // each lane carries the utterance and running delta of its last finding in this chunk
+        const bool here = nf && incl > f0 && excl < f0 + 64;
+        const int last = here ? (int)(min(incl, f0 + 64) - 1 - f0) : 0;
+        const uint32_t lu = __shfl(uk, last);
+        const int64_t lrun = __shfl(base + sc, last);
+        if (here) {
+            carry_u = lu;
+            carry_run = lrun;
         }
     }
     __syncthreads();
