@@ -135,6 +135,26 @@ def test_edge_cases(eng, oracle_cfg):
     assert list(allempty.out_offsets) == [0] * 6
 
 
+def test_dense_findings_per_lane(eng, oracle_cfg):
+    """more than 64 findings in one scan lane and in one utterance (k_spans / k_select carry their
+    running state across 64-finding chunks), beside rows with none"""
+    from oracle import pii_oracle as O
+    r = random.Random(41)
+    texts = []
+    for k in range(60):
+        n = r.randrange(40, 400)
+        items = [f"u{r.randrange(10 ** 6)}@x{r.randrange(9)}.io" if r.random() < 0.7 else
+                 f"10.{r.randrange(256)}.{r.randrange(256)}.{r.randrange(256)}" for _ in range(n)]
+        texts.append(" ".join(items).encode())
+        texts.append(b"ok thanks" if k % 3 else b"")
+    res = eng.scan_redact(texts, list(range(30000, 30000 + len(texts))), [O.ROLE_CUSTOMER] * len(texts))
+    assert max(len(_spans_of(res, i)) for i in range(len(texts))) > 128
+    for i, t in enumerate(texts):
+        red, fs = O.redact(t, oracle_cfg, None)
+        assert res.text(i) == red, (i, t[:60])
+        assert _spans_of(res, i) == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], i
+
+
 def test_context_ttl_and_persistence(eng, oracle_cfg):
     from oracle import pii_oracle as O
     E = pkg("engine")
