@@ -77,9 +77,16 @@ class MicroBatcher:
                 res = self.service.process_requests([(k, d) for k, d, _ in batch])
                 for (_, _, f), r in zip(batch, res):
                     f.set_result(r)
-            except Exception as e:              # never leave a request thread waiting
-                for _, _, f in batch:
-                    if not f.done():
+            except Exception:
+                # a failure that request validation did not foresee: rerun the batch one request at
+                # a time so that only the request that raises fails (as it would alone in the
+                # reference's per-request handler), and never leave a request thread waiting
+                for k, d, f in batch:
+                    if f.done():
+                        continue
+                    try:
+                        f.set_result(self.service.process_requests([(k, d)])[0])
+                    except Exception as e:
                         f.set_exception(e)
             if stop:
                 return

@@ -704,6 +704,9 @@ class Rules:
         for n in self.base_info_types + self.custom_names + list(dets.keys()) + list(self.context_keywords):
             if n not in order:
                 order.append(n)
+        # types of external detectors (the NER): last in the type order, no pattern, no variant
+        self.external_types = [n for n in (builtin.get("external_types") or []) if n not in order]
+        order += self.external_types
         self.type_names = order
         self.type_id = {n: i for i, n in enumerate(order)}
         self.patterns: List[Pattern] = []
@@ -742,7 +745,7 @@ class Rules:
         # (config 5) skip this: V * T variant tables would not fit the kernels' LDS images.
         self.n_keyword_groups = len(self.kw_groups)
         if len(self.type_names) <= PSEUDO_GROUP_MAX_TYPES:
-            named = {t for t, _, _ in self.kw_groups}
+            named = {t for t, _, _ in self.kw_groups} | set(self.external_types)
             self.kw_groups.extend((t, None, False) for t in self.type_names if t not in named)
 
     @classmethod
@@ -992,7 +995,7 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
     for v, insp in enumerate(rules.variants()):
         enabled = {it.get("name") for it in insp.get("info_types", [])}
         enabled |= {c.get("info_type", {}).get("name") for c in insp.get("custom_info_types", []) or []}
-        for name in enabled:
+        for name in list(enabled) + rules.external_types:
             if name in rules.type_id:
                 var_enabled[v, rules.type_id[name]] = 1
         var_minlik[v] = lik_value(insp.get("min_likelihood", DEFAULT_MIN_LIKELIHOOD))
@@ -1025,6 +1028,10 @@ def compile_rules(rules: Rules, scan_budget: int = SCAN_BUDGET) -> Compiled:
                     for tn in tnames:
                         if tn in rules.type_id:
                             per_type_excl[rules.type_id[tn]].extend(rules.type_id[x] for x in xs if x in rules.type_id)
+        for x in rules.external_types:
+            xt = rules.type_id[x]
+            if per_type_rules[xt] or per_type_excl[xt] or any(xt in l for l in per_type_excl):
+                raise RuleError(f"external type {x} cannot be named by a hotword or exclusion rule")
         for t in range(T):
             rule_ids.extend(per_type_rules[t])
             rule_off[v * T + t + 1] = len(rule_ids)

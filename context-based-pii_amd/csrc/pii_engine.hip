@@ -50,7 +50,7 @@ constexpr int KW_NONE = 0x7fff;
 constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
 
 enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16, ERR_STITCH = 32,
-                  ERR_ARGS = 64 };
+                  ERR_ARGS = 64, ERR_EXT = 128 };
 // a call whose declared batch size was wrong (ERR_ARGS) or whose queues overflowed (ERR_QUEUE, re-run by
 // pii_sync) stops every later stage
 constexpr uint32_t ERR_ABORT = ERR_QUEUE | ERR_ARGS;
@@ -1825,6 +1825,12 @@ struct SelIO {
     uint32_t* lane_reach;   // lanes cut at hi: furthest match end of the cut row (row relative)
     uint32_t* out_len;
     uint2* spill;           // per pair-queue index: the (pattern, end) list of a run past LIVE patterns
+    // external candidates (another detector's spans, e.g. the NER's PERSON_NAME): ext[row * ext_stride
+    // + k] for k < ext_n[row], row-relative, sorted by start; only read by select_run<true>
+    const pii_span* ext;
+    const uint32_t* ext_n;
+    uint32_t ext_stride;
+    uint32_t* err;          // ERR_EXT: a malformed external span
 };
 
 __device__ __forceinline__ uint64_t fd_base(const Lane& L, uint32_t c, int min_len) {
@@ -1843,7 +1849,11 @@ __device__ __forceinline__ SelTabs sel_tabs(const uint8_t* lb, const LdsImage& l
     return T;
 }
 
-// select over the pairs of lanes c0..c1 as ONE sequential pass (the state carries across the lanes)
+// select over the pairs of lanes c0..c1 as ONE sequential pass (the state carries across the lanes).
+// EXT: the lanes' external candidates (SelIO::ext) are merged into the pair stream in (row, start)
+// order; they take part in overlap resolution (A.6) and min_likelihood like any finding, but not in
+// finditer skipping (they have no pattern) nor as excluders.
+template <bool EXT>
 __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t c0,
                            uint32_t c1) {
     const int T = R.T;
@@ -1900,14 +1910,14 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     auto flush_utt = [&]() {
         if (nf_u) io.out_len[u] += (uint32_t)delta_u;      // (k_chunk_index wrote the row length)
     };
-    auto pair = [&](const SelRec& P, int e) {
-        const int ps = P.ps;
-        if (P.u != u) {
+    // candidate (row pu, start ps, end e) enters: row / start transitions
+    auto enter = [&](uint32_t pu, int ps, int e) {
+        if (pu != u) {
             if (u != 0xffffffffu) {
                 flush_start();
                 flush_utt();
             }
-            u = P.u;
+            u = pu;
             v = (io.role[u] == PII_ROLE_CUSTOMER && io.ctx[u] >= 0) ? io.ctx[u] + 1 : 0;
             minlik = Tb.vmin[v];
 #pragma unroll
@@ -1927,6 +1937,29 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             s = ps;
         }
         if (Lg.chi && u == Lg.u1 - 1) reach = max(reach, (uint32_t)e);
+    };
+    // a valid candidate of type t (excluder slot xi, 0xff: none) competes for its start
+    auto consider = [&](int t, int lik, int e, int xi) {
+        const uint32_t x0 = Tb.xoff[v * T + t], x1 = Tb.xoff[v * T + t + 1];
+        bool excluded = false;
+        for (uint32_t q = x0; q < x1; ++q) {
+            const int xt = Tb.xids[q];
+#pragma unroll
+            for (int x = 0; x < NE_MAX; ++x)
+                if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
+                    excluded = true;
+        }
+        if (excluded) return;
+        const bool better = best_e < 0 || e > best_e ||
+                            (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
+        if (better) {
+            best_e = e;
+            best_t = t;
+            best_lik = lik;
+        }
+    };
+    auto pair = [&](const SelRec& P, int e) {
+        enter(P.u, P.ps, e);
         const int p = P.p;
         const int t = Tb.dtype[p];
         if (!Tb.ven[v * T + t]) return;
@@ -1987,23 +2020,57 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 }
             ex_valid |= 1u << xi;
         }
-        const uint32_t x0 = Tb.xoff[v * T + t], x1 = Tb.xoff[v * T + t + 1];
-        bool excluded = false;
-        for (uint32_t q = x0; q < x1; ++q) {
-            const int xt = Tb.xids[q];
-#pragma unroll
-            for (int x = 0; x < NE_MAX; ++x)
-                if (x != xi && ((ex_valid >> x) & 1) && ex_t[x] == xt && ex_s[x] <= s && e <= ex_e[x])
-                    excluded = true;
+        consider(t, lik, e, xi);
+    };
+    // external candidates: cursor over the lane's rows [u0, u1); a cut row contributes the spans
+    // whose start lies in the lane's byte range.  Every span is checked (start < end <= row length,
+    // sorted by start, type < T, likelihood 1..5); a bad one sets ERR_EXT and is skipped.
+    uint32_t xu = 0, xk = 0, xn = 0, xprev = 0;
+    pii_span X{};
+    bool xhave = false;
+    auto xrow = [&](uint32_t r) {
+        xu = r;
+        xk = 0;
+        xprev = 0;
+        xn = 0;
+        if (r < Lg.u1) {
+            xn = io.ext_n[r];
+            if (xn > io.ext_stride) {
+                atomicOr(io.err, ERR_EXT);
+                xn = io.ext_stride;
+            }
         }
-        if (excluded) return;
-        const bool better = best_e < 0 || e > best_e ||
-                            (e == best_e && (lik > best_lik || (lik == best_lik && t < best_t)));
-        if (better) {
-            best_e = e;
-            best_t = t;
-            best_lik = lik;
+    };
+    auto xload = [&]() {
+        xhave = false;
+        while (xu < Lg.u1) {
+            if (xk < xn) {
+                X = io.ext[(uint64_t)xu * io.ext_stride + xk++];
+                const int64_t r0 = g_off(g, xu), rl = g_off(g, xu + 1) - r0;
+                if (X.end <= X.start || (int64_t)X.end > rl || X.start < xprev || (int)X.info_type >= T ||
+                    X.likelihood == 0 || X.likelihood > 5) {
+                    atomicOr(io.err, ERR_EXT);
+                    continue;
+                }
+                xprev = X.start;
+                const int64_t a = r0 + X.start;
+                if (Lg.clo && xu == Lg.u0 && a < (int64_t)Lg.lo) continue;
+                if (Lg.chi && xu == Lg.u1 - 1 && a >= (int64_t)Lg.hi) {
+                    xk = xn;
+                    continue;
+                }
+                X.utt = xu;
+                xhave = true;
+                return;
+            }
+            xrow(xu + 1);
         }
+    };
+    auto ext_cand = [&]() {
+        const int e = (int)X.end, t = X.info_type, lik = X.likelihood;
+        enter(X.utt, (int)X.start, e);
+        if (Tb.ven[v * T + t] && lik >= minlik) consider(t, lik, e, 0xff);
+        xload();
     };
     for (lane = c0; lane <= c1; ++lane) {
         Lg = g_lane(g, lane);
@@ -2011,6 +2078,10 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
         nfl = 0;
         rdx = rdy = 0;
         reach = 0;
+        if (EXT) {
+            xrow(Lg.u0);
+            xload();
+        }
         const uint32_t np = io.lane_np[lane];
         const uint64_t pbase = io.lane_pair[lane];
         if (np && pbase + np <= io.pair_cap) {
@@ -2054,9 +2125,13 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 const int e = el[i1];          // (in L1: its group was just loaded)
                 ok = adv(i1);
                 if (ok) r1 = io.sel[pbase + i1];
+                if (EXT)
+                    while (xhave && (X.utt < r.u || (X.utt == r.u && (int)X.start <= r.ps))) ext_cand();
                 pair(r, e);
             }
         }
+        if (EXT)
+            while (xhave) ext_cand();
         // the pending start and (unless the row continues into the next lane) the utterance end here
         if (u != 0xffffffffu) {
             flush_start();
@@ -2071,7 +2146,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     }
 }
 
-template <bool GI>
+template <bool GI, bool EXT>
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 const Geo g, const SelIO io, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
@@ -2080,7 +2155,7 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
     const SelTabs Tb = sel_tabs(lb, li);
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= g.n_chunks) return;
-    select_run(R, Tb, g, io, c, c);
+    select_run<EXT>(R, Tb, g, io, c, c);
 }
 
 // ---- cut rows: which continuation lanes need the carried state (a match of an earlier lane of the
@@ -2136,7 +2211,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint
 }
 
 // re-run every maximal chain of dirty lanes from the clean lane before it (one thread per chain)
-template <bool GI>
+template <bool GI, bool EXT>
 __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                  const Geo g, const SelIO io, const uint32_t* __restrict__ long_rows,
                                                  const uint32_t* __restrict__ long_count,
@@ -2153,7 +2228,7 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
             if (dirty[j] || !dirty[j + 1]) continue;
             uint32_t c = j + 1;
             while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
-            select_run(R, Tb, g, io, j, c);
+            select_run<EXT>(R, Tb, g, io, j, c);
         }
     }
 }
@@ -3724,6 +3799,9 @@ struct pii_engine {
         uint32_t span_cap;
         int16_t* ctx_info;
         hipStream_t st;
+        const pii_span* ext;
+        const uint32_t* ext_n;
+        uint32_t ext_stride;
     } last{};
     int32_t* kw = nullptr;
     int16_t* ctx = nullptr;
@@ -3746,6 +3824,10 @@ struct pii_engine {
     int64_t* h_ts = nullptr;
     pii_span* h_spans = nullptr;
     int16_t* h_ctx = nullptr;
+    pii_span* h_ext = nullptr;         // external candidates of a host-buffer call
+    uint32_t* h_ext_n = nullptr;
+    uint64_t cap_h_ext = 0;
+    uint32_t cap_h_ext_n = 0;
     hipEvent_t tev[7] = {};
     float last_ms[6] = {};
     hipEvent_t kev[4] = {};           // around k_scan and k_redact (the roofline kernels)
@@ -3823,11 +3905,12 @@ int grow_pairs(pii_engine* e, uint64_t cap) {
     return PII_OK;
 }
 
-int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lanes) {
+int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lanes, int min_len = 0) {
     int rc = PII_OK;
     // event arenas: a lane's emitted positions + its utterance starts (ev_base); findings arenas:
-    // one finding per min_len bytes + one per lane (fd_base)
-    const uint64_t need_ev = bytes + n_utt + n_lanes + 2, need_fd = bytes / e->R.min_len + n_lanes + 2;
+    // one finding per min_len bytes + one per lane (fd_base; min_len 1 when external spans come in)
+    if (min_len <= 0) min_len = e->R.min_len;
+    const uint64_t need_ev = bytes + n_utt + n_lanes + 2, need_fd = bytes / (uint64_t)min_len + n_lanes + 2;
     if (need_ev > e->cap_ev) {           // one arena per SCAN group, cap_ev events apart
         const uint64_t nb = std::max<uint64_t>(need_ev + need_ev / 8, 1 << 16);
         if ((rc = grow(e, e->ev, nb * e->n_sg))) return rc;
@@ -4093,9 +4176,15 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
 int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
                  uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out,
                  uint64_t out_cap, uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info,
-                 hipStream_t st) {
+                 hipStream_t st, const pii_span* ext = nullptr, const uint32_t* ext_n = nullptr,
+                 uint32_t ext_stride = 0) {
     if (total_bytes > PII_MAX_BATCH_BYTES || total_bytes + 2ull * n_utt + (total_bytes >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
+        return PII_E_ARG;
+    }
+    const bool has_ext = ext != nullptr && n_utt > 0;
+    if (has_ext && (!ext_n || ext_stride == 0)) {
+        e->err = "external spans need their per-row counts and a stride > 0";
         return PII_E_ARG;
     }
     e->lane_shift = pick_lane_shift(e, total_bytes);
@@ -4103,10 +4192,13 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     e->long_min = 2u << e->lane_shift;          // rows longer than two lanes are cut
     const uint32_t n_chunks = lane_count(e, total_bytes);
     e->last_lanes = n_chunks;
-    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
+    // external spans can be 1 byte long: the findings arenas are sized (and placed) for that
+    RulesDev Rsel = e->R;
+    if (has_ext) Rsel.min_len = 1;
+    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks, Rsel.min_len);
     if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_redact(e, span_cap, out_cap))) return rc;
     e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
-                               span_cap, ctx_info, st};
+                               span_cap, ctx_info, st, ext, ext_n, ext_stride};
     e->last_kind = 0;
     const RulesDev& R = e->R;
     int16_t* ctx = ctx_info ? ctx_info : e->ctx;
@@ -4124,13 +4216,17 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
             e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont));
         const SelIO io{e->lane_pair, e->lane_np, reinterpret_cast<const SelRec*>(e->cont), e->pend, e->pair_cap, role, ctx, e->fd,
-                       e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill};
-        (e->img_sel.global ? k_select<true> : k_select<false>)<<<(n_chunks + 255) / 256, 256, e->img_sel.lds(), st>>>(
-            R, e->img_sel.d, e->img_sel.li, g, io, e->d_err);
+                       e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill, ext, ext_n, ext_stride, e->d_err};
+        const bool gi = e->img_sel.global;
+        auto ksel = has_ext ? (gi ? k_select<true, true> : k_select<false, true>)
+                            : (gi ? k_select<true, false> : k_select<false, false>);
+        auto kfix = has_ext ? (gi ? k_sel_fix<true, true> : k_sel_fix<false, true>)
+                            : (gi ? k_sel_fix<true, false> : k_sel_fix<false, false>);
+        ksel<<<(n_chunks + 255) / 256, 256, e->img_sel.lds(), st>>>(Rsel, e->img_sel.d, e->img_sel.li, g, io, e->d_err);
         const uint32_t rg = row_grid(e, total_bytes);
         k_sel_dirty<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_reach, e->dirty, e->d_err);
-        (e->img_sel.global ? k_sel_fix<true> : k_sel_fix<false>)<<<rg, 256, e->img_sel.lds(), st>>>(
-            R, e->img_sel.d, e->img_sel.li, g, io, e->long_rows, e->long_count, e->dirty, e->d_err);
+        kfix<<<rg, 256, e->img_sel.lds(), st>>>(Rsel, e->img_sel.d, e->img_sel.li, g, io, e->long_rows, e->long_count,
+                                                 e->dirty, e->d_err);
         k_rowlen<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_rd, e->lane_rowbase, e->out_len,
                                           e->d_err);
         HIPCHK(hipGetLastError());
@@ -4145,7 +4241,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     if (n_utt > 0) {
         if (n_chunks > 0) {
             const uint32_t nsb = (n_chunks + 255) / 256;
-            k_spans<<<nsb, 256, 0, st>>>(R, g, e->fd, e->lane_nf, e->lane_sp, e->lane_rowbase, out_offs, e->d_err,
+            k_spans<<<nsb, 256, 0, st>>>(Rsel, g, e->fd, e->lane_nf, e->lane_sp, e->lane_rowbase, out_offs, e->d_err,
                                          spans, e->rsp, e->hist_part, e->hist_types);
             const uint32_t tiles = (uint32_t)((out_cap + 15) >> RTILE_SHIFT) + 1;
             k_tile_first<<<(tiles + 255) / 256, 256, 0, st>>>(R, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
@@ -4275,13 +4371,18 @@ int rerun_last(pii_engine* e) {
         return run_window(e, c.text, c.offs, c.n_utt, c.base, c.total, c.slot, c.role, c.ts, c.out, c.out_cap,
                           c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st);
     return run_pipeline(e, c.text, c.offs, c.n_utt, c.base, c.total, c.slot, c.role, c.ts, c.out, c.out_cap,
-                        c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st);
+                        c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st, c.ext, c.ext_n, c.ext_stride);
 }
 
+struct ExtArgs {
+    const pii_span* ext;
+    const uint32_t* ext_n;
+    uint32_t stride;
+};
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
                 const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
                 uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream,
-                const uint64_t* declared);
+                const uint64_t* declared, const ExtArgs* x = nullptr);
 }  // namespace
 
 extern "C" {
@@ -4613,7 +4714,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->wsel_ok = !e->img_wsel.global && !e->img_eval.global;
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first<false>, &e->img_first}, {(const void*)k_pair_eval<false>, &e->img_eval},
-            {(const void*)k_select<false>, &e->img_sel}, {(const void*)k_sel_fix<false>, &e->img_sel},
+            {(const void*)k_select<false, false>, &e->img_sel}, {(const void*)k_sel_fix<false, false>, &e->img_sel},
+            {(const void*)k_select<false, true>, &e->img_sel}, {(const void*)k_sel_fix<false, true>, &e->img_sel},
             {(const void*)k_win_eval, &e->img_eval},
             {(const void*)k_win_select, &e->img_wsel}, {(const void*)k_win_halo, &e->img_eval}};
         for (auto& kb : big)
@@ -4709,7 +4811,7 @@ int pii_engine_destroy(pii_engine* e) {
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
                     e->long_rows, e->lane_st, e->lane_geo, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
-                    e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first};
+                    e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first, e->h_ext, e->h_ext_n};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
@@ -4838,6 +4940,11 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         return PII_E_ARG;
     }
     if (f & ERR_SLOT) return PII_E_ARG;
+    if (f & ERR_EXT) {
+        e->err = "an external span is malformed (start < end <= row length, sorted by start, info_type < n_types, "
+                 "likelihood 1..5, ext_n <= ext_stride)";
+        return PII_E_ARG;
+    }
     if (f & ERR_RING) {
         e->err = "a conversation's re-scan window does not fit its history slot; raise slot_bytes (pii_window_enable)";
         return PII_E_NOMEM;
@@ -4890,8 +4997,9 @@ namespace {
 int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
               const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
               uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
-              int16_t* ctx_info) {
+              int16_t* ctx_info, const ExtArgs* x = nullptr) {
     if (!e || !offsets || !out_offsets || (n_utt && (!conv_slot || !role))) return PII_E_ARG;
+    if (x && (!x->ext || !x->ext_n || x->stride == 0)) return PII_E_ARG;
     for (uint32_t i = 0; i < n_utt; ++i)
         if (offsets[i + 1] < offsets[i]) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
@@ -4930,9 +5038,26 @@ int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* 
         HIPCHK(hipMemcpyAsync(e->h_role, role, n_utt, hipMemcpyHostToDevice, st));
         if (ts_us) HIPCHK(hipMemcpyAsync(e->h_ts, ts_us, n_utt * 8, hipMemcpyHostToDevice, st));
     }
-    rc = (window ? run_window : run_pipeline)(e, e->h_text, e->h_offs, n_utt, 0, total, e->h_slot, e->h_role,
-                                              ts_us ? e->h_ts : nullptr, e->h_out, out_cap, e->h_out_offs, e->h_spans,
-                                              span_cap, e->h_ctx, st);
+    if (x && n_utt) {          // stage the external spans (stride-padded rows) next to the text
+        const uint64_t ne = (uint64_t)n_utt * x->stride;
+        if (ne > e->cap_h_ext) {
+            if ((rc = grow(e, e->h_ext, ne))) return rc;
+            e->cap_h_ext = ne;
+        }
+        if (n_utt > e->cap_h_ext_n) {
+            if ((rc = grow(e, e->h_ext_n, (size_t)n_utt + n_utt / 8 + 64))) return rc;
+            e->cap_h_ext_n = n_utt + n_utt / 8 + 64;
+        }
+        HIPCHK(hipMemcpyAsync(e->h_ext, x->ext, ne * sizeof(pii_span), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->h_ext_n, x->ext_n, (size_t)n_utt * 4, hipMemcpyHostToDevice, st));
+    }
+    if (window)
+        rc = run_window(e, e->h_text, e->h_offs, n_utt, 0, total, e->h_slot, e->h_role, ts_us ? e->h_ts : nullptr,
+                        e->h_out, out_cap, e->h_out_offs, e->h_spans, span_cap, e->h_ctx, st);
+    else
+        rc = run_pipeline(e, e->h_text, e->h_offs, n_utt, 0, total, e->h_slot, e->h_role, ts_us ? e->h_ts : nullptr,
+                          e->h_out, out_cap, e->h_out_offs, e->h_spans, span_cap, e->h_ctx, st,
+                          x ? e->h_ext : nullptr, x ? e->h_ext_n : nullptr, x ? x->stride : 0);
     if (rc) return rc;
     uint64_t tot[3];
     rc = pii_sync(e, tot);
@@ -4953,7 +5078,7 @@ int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* 
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
                 const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
                 uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream,
-                const uint64_t* declared = nullptr) {
+                const uint64_t* declared, const ExtArgs* x) {
     if (!e || !d_offsets || !d_slot || !d_role || !d_out_offsets) return PII_E_ARG;
     if (n_utt > 0 && (!d_bytes || !d_out || !d_spans)) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
@@ -4968,8 +5093,12 @@ int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64
         HIPCHK(hipStreamSynchronize(st));
     }
     if (tb[1] < tb[0]) return PII_E_ARG;
-    return (window ? run_window : run_pipeline)(e, d_bytes, d_offsets, n_utt, tb[0], tb[1] - tb[0], d_slot, d_role,
-                                                d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx_info, st);
+    if (window)
+        return run_window(e, d_bytes, d_offsets, n_utt, tb[0], tb[1] - tb[0], d_slot, d_role, d_ts, d_out, out_cap,
+                          d_out_offsets, d_spans, span_cap, d_ctx_info, st);
+    return run_pipeline(e, d_bytes, d_offsets, n_utt, tb[0], tb[1] - tb[0], d_slot, d_role, d_ts, d_out, out_cap,
+                        d_out_offsets, d_spans, span_cap, d_ctx_info, st, x ? x->ext : nullptr, x ? x->ext_n : nullptr,
+                        x ? x->stride : 0);
 }
 }  // namespace
 
@@ -4981,6 +5110,27 @@ int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets
                     int16_t* ctx_info) {
     return host_call(e, false, bytes, offsets, n_utt, conv_slot, role, ts_us, out_bytes, out_cap, out_offsets, spans,
                      span_cap, n_spans, ctx_info);
+}
+
+int pii_scan_redact_ext(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                        const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
+                        uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
+                        int16_t* ctx_info, const pii_span* ext, const uint32_t* ext_n, uint32_t ext_stride) {
+    const ExtArgs x{ext, ext_n, ext_stride};
+    return host_call(e, false, bytes, offsets, n_utt, conv_slot, role, ts_us, out_bytes, out_cap, out_offsets, spans,
+                     span_cap, n_spans, ctx_info, &x);
+}
+
+int pii_scan_redact_device_ext(pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
+                               uint64_t batch_base, uint64_t batch_bytes, const uint32_t* d_slot, const uint8_t* d_role,
+                               const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_offsets,
+                               pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, const pii_span* d_ext,
+                               const uint32_t* d_ext_n, uint32_t ext_stride, void* stream) {
+    if (!d_ext || !d_ext_n || ext_stride == 0) return PII_E_ARG;
+    const uint64_t decl[2] = {batch_base, batch_bytes};
+    const ExtArgs x{d_ext, d_ext_n, ext_stride};
+    return device_call(e, false, d_bytes, d_offsets, n_utt, d_slot, d_role, d_ts, d_out, out_cap, d_out_offsets,
+                       d_spans, span_cap, d_ctx_info, stream, decl, &x);
 }
 
 int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
@@ -5090,10 +5240,13 @@ int pii_histogram(pii_engine* e, uint64_t* counts, uint32_t n) {
     return PII_OK;
 }
 
-// stream-ordered: the next call on the engine's stream starts from zero (no host wait here)
+// stream-ordered: the next call on the engine's stream starts from zero (no host wait here). The
+// memset first waits for the last call's end event, which that call recorded on ITS stream (a
+// caller stream for the _ex entry points), so the reset never races that call's k_hist_reduce.
 int pii_histogram_reset(pii_engine* e) {
     if (!e) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamWaitEvent(e->stream, e->tev[6], 0));
     HIPCHK(hipMemsetAsync(e->hist, 0, std::max(e->R.T, 256) * 8, e->stream));
     e->h_hist_valid = false;
     e->reset_pending = true;

@@ -26,7 +26,7 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
-           "pii_rescan_window_device_ex"]
+           "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext"]
 
 
 class PiiError(RuntimeError):
@@ -83,6 +83,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_scan_redact_device.argtypes = [P, P, P, c.c_uint32, P, P, P, P, c.c_uint64, P, P, c.c_uint32, P, P]
     lib.pii_scan_redact_device_ex.argtypes = [P, P, P, c.c_uint32, c.c_uint64, c.c_uint64, P, P, P, P, c.c_uint64,
                                               P, P, c.c_uint32, P, P]
+    lib.pii_scan_redact_ext.argtypes = lib.pii_scan_redact.argtypes + [P, P, c.c_uint32]
+    lib.pii_scan_redact_device_ext.argtypes = lib.pii_scan_redact_device_ex.argtypes[:-1] + [P, P, c.c_uint32, P]
     lib.pii_reserve.argtypes = [P, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32]
     lib.pii_sync.argtypes = [P, U64]
     lib.pii_context_get.argtypes = [P, c.c_uint32, I32, I64]
@@ -116,6 +118,21 @@ def pack(texts: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
     np.cumsum(lens, out=offs[1:])
     data = np.frombuffer(b"".join(texts), dtype=np.uint8) if len(texts) else np.zeros(0, np.uint8)
     return data, offs
+
+
+def ext_arrays(ext: Sequence[Sequence[tuple]], n: int) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Per-row candidate lists [(start, end, info_type, likelihood)] -> (pii_span rows padded to one
+    stride, counts uint32[n], stride), the layout of pii_scan_redact_ext."""
+    if len(ext) != n:
+        raise ValueError("one external candidate list per row")
+    stride = max(1, max((len(x) for x in ext), default=0))
+    spans = np.zeros(n * stride, dtype=SPAN_DTYPE)
+    counts = np.zeros(max(1, n), dtype=np.uint32)
+    for i, xs in enumerate(ext):
+        counts[i] = len(xs)
+        for k, (s, e, t, lik) in enumerate(xs):
+            spans[i * stride + k] = (i, s, e, t, lik, 0)
+    return spans, counts, stride
 
 
 @dataclass
@@ -180,8 +197,15 @@ class Engine:
 
     # ------------------------------------------------------------------ host-buffer batch API
     def scan_redact(self, texts: Sequence[bytes], conv_slot: Sequence[int], role: Sequence[int],
-                    ts_us: Optional[Sequence[int]] = None) -> BatchResult:
-        return self._host_call(self.lib.pii_scan_redact, "pii_scan_redact", texts, conv_slot, role, ts_us, 1)
+                    ts_us: Optional[Sequence[int]] = None, ext: Optional[Sequence[Sequence[tuple]]] = None
+                    ) -> BatchResult:
+        """ext[i]: row i's external-detector candidates [(start, end, info_type, likelihood)], sorted by
+        start (pii_scan_redact_ext: they join overlap resolution with the rule findings)."""
+        if ext is None:
+            return self._host_call(self.lib.pii_scan_redact, "pii_scan_redact", texts, conv_slot, role, ts_us, 1)
+        spans, counts, stride = ext_arrays(ext, len(texts))
+        fn = lambda *a: self.lib.pii_scan_redact_ext(*a, _ptr(spans), _ptr(counts), stride)   # noqa: E731
+        return self._host_call(fn, "pii_scan_redact_ext", texts, conv_slot, role, ts_us, 1)
 
     def rescan_window(self, texts: Sequence[bytes], conv_slot: Sequence[int], role: Sequence[int],
                       ts_us: Optional[Sequence[int]] = None) -> BatchResult:
@@ -268,6 +292,17 @@ class Engine:
                                                 stream)
         if rc != PII_OK:
             raise self._err(rc, "pii_scan_redact_device_ex")
+
+    def scan_redact_device_ext(self, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot, d_role, d_ts, d_out,
+                               out_cap, d_out_offsets, d_spans, span_cap, d_ctx, d_ext, d_ext_n, ext_stride,
+                               stream=None) -> None:
+        """scan_redact_device_ex plus external candidates in device memory (pii_scan_redact_device_ext):
+        d_ext[row * ext_stride + k] for k < d_ext_n[row]."""
+        rc = self.lib.pii_scan_redact_device_ext(self.h, d_bytes, d_offsets, n_utt, batch_base, batch_bytes, d_slot,
+                                                 d_role, d_ts, d_out, out_cap, d_out_offsets, d_spans, span_cap, d_ctx,
+                                                 d_ext, d_ext_n, ext_stride, stream)
+        if rc != PII_OK:
+            raise self._err(rc, "pii_scan_redact_device_ext")
 
     def reserve(self, max_utt: int, max_bytes: int, max_out: int, max_spans: int) -> None:
         """pre-size the work buffers so calls within these bounds allocate nothing (pii_reserve)"""

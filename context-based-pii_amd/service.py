@@ -250,6 +250,30 @@ class PiiService:
 
     REQUEST_KEYS = {"agent": "transcript", "customer": "transcript", "realtime": "utterance"}
 
+    @classmethod
+    def request_error(cls, kind: str, data) -> Optional[Tuple[dict, int]]:
+        """The response a request gets on its own, before any engine call, or None when it is
+        well-formed.  A body without the two keys is the reference's 400 (main.py:351-352,
+        393-394, 434-435).  A body the reference's handler would crash on after that check -- a
+        JSON string (``data['conversation_id']`` on a str), a non-string text (``.lower()`` in
+        extract_expected_pii, the f-string join of main.py:457) or an unhashable id (the Redis key
+        is built from it, here the slot map) -- is that request's own 500, never its batch's."""
+        key = cls.REQUEST_KEYS[kind]
+        missing = ({"error": f"Missing conversation_id or {key}"}, 400)
+        if not data:
+            return missing
+        if not isinstance(data, (dict, list, str)):           # `key in 5` raises in the reference
+            return ({"error": "Internal Server Error"}, 500)
+        if "conversation_id" not in data or key not in data:
+            return missing
+        if not isinstance(data, dict) or not isinstance(data[key], str):
+            return ({"error": "Internal Server Error"}, 500)
+        try:
+            hash(data["conversation_id"])
+        except TypeError:
+            return ({"error": "Internal Server Error"}, 500)
+        return None
+
     def process_requests(self, reqs: Sequence[Tuple[str, Optional[dict]]]) -> List[Tuple[dict, int]]:
         """A micro-batch of handler requests [(kind, json body)] in arrival order, kind in
         {"agent", "customer", "realtime"} (/handle-agent-utterance, /handle-customer-utterance,
@@ -263,9 +287,9 @@ class PiiService:
         out: List[Optional[Tuple[dict, int]]] = [None] * len(reqs)
         valid = []
         for i, (kind, data) in enumerate(reqs):
-            key = self.REQUEST_KEYS[kind]
-            if not data or "conversation_id" not in data or key not in data:
-                out[i] = ({"error": f"Missing conversation_id or {key}"}, 400)
+            err = self.request_error(kind, data)
+            if err is not None:
+                out[i] = err
             else:
                 valid.append(i)
         split, agents, cur_convs = [], set(), set()

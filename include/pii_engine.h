@@ -119,6 +119,28 @@ int pii_scan_redact_device_ex(struct pii_engine* e, const uint8_t* d_bytes, cons
                               const uint32_t* d_conv_slot, const uint8_t* d_role, const int64_t* d_ts_us,
                               uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets,
                               pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream);
+/* External candidates: the findings of a detector outside the rules blob -- the
+ * optional NER (libner.so, ner.py) and its PERSON_NAME, the detector the "full name|your name" hotword
+ * of main_service/dlp_config.yaml:170 asks for and no configured detector provides.  Row i's
+ * candidates are ext[i * ext_stride + k] for k < ext_n[i] (<= ext_stride): start / end row-relative
+ * byte offsets, sorted by start, info_type < n_types (normally one of the rules' external types,
+ * rules/builtin_infotypes.yaml `external_types`), likelihood 1..5; utt and flags are ignored.  They
+ * join the rule findings in overlap resolution -- after validation and hotwords, subject
+ * to min_likelihood and the context variant's enabled types, never as excluders -- so they reach the
+ * span list, the redacted bytes ("[PERSON_NAME]") and the histogram like any finding.  A malformed
+ * span fails the call with PII_E_ARG (nothing committed).  Otherwise identical to
+ * pii_scan_redact / pii_scan_redact_device_ex. */
+int pii_scan_redact_ext(struct pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                        const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us,
+                        uint8_t* out_bytes, uint64_t out_cap, uint64_t* out_offsets,
+                        pii_span* spans, uint32_t span_cap, uint32_t* n_spans, int16_t* ctx_info,
+                        const pii_span* ext, const uint32_t* ext_n, uint32_t ext_stride);
+int pii_scan_redact_device_ext(struct pii_engine* e, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                               uint32_t n_utt, uint64_t batch_base, uint64_t batch_bytes,
+                               const uint32_t* d_conv_slot, const uint8_t* d_role, const int64_t* d_ts_us,
+                               uint8_t* d_out_bytes, uint64_t out_cap, uint64_t* d_out_offsets,
+                               pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info,
+                               const pii_span* d_ext, const uint32_t* d_ext_n, uint32_t ext_stride, void* stream);
 /* Pre-size every internal work buffer for batches of at most max_utt rows / max_bytes input bytes /
  * max_out output bytes / max_spans spans, so that calls within those bounds allocate nothing (no
  * hipMalloc, which synchronizes the device, inside a streaming loop).  The pair / event queues still

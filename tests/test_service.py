@@ -442,6 +442,52 @@ def test_flask_routes_shapes_and_microbatching(oracle_cfg):
     app.config["PII_BATCHER"].close()
 
 
+def test_malformed_request_fails_alone(oracle_cfg):
+    """A body the reference's handler would crash on is that request's own error, never its
+    micro-batch's: the well-formed requests batched with it get their sequential answers."""
+    S = pkg("service")
+    make = lambda: S.PiiService(engine=OracleEngine(oracle_cfg, n_slots=32), clock=Clock())
+    good = [("agent", {"conversation_id": "g1", "transcript": "What is your email address?"}),
+            ("customer", {"conversation_id": "g1", "transcript": "it is jane.doe@example.com"}),
+            ("customer", {"conversation_id": "g2", "transcript": "my ssn is 123-45-6789"})]
+    bad = [("customer", ["conversation_id", "transcript"]),                 # JSON list body
+           ("customer", "conversation_id transcript"),                     # JSON string body
+           ("agent", {"conversation_id": "b", "transcript": None}),         # null text
+           ("customer", {"conversation_id": "b", "transcript": 7}),         # non-string text
+           ("realtime", {"conversation_id": ["x"], "utterance": "hi"}),     # unhashable id
+           ("agent", 5),                                                    # number body
+           ("agent", {"conversation_id": "b"})]                             # missing key -> 400
+    mixed = [good[0], bad[0], bad[1], good[1], bad[2], bad[3], bad[4], good[2], bad[5], bad[6]]
+    got = make().process_requests(mixed)
+    want_good = _sequential(make, good)
+    assert [got[0], got[3], got[7]] == want_good
+    assert [got[i][1] for i in (1, 2, 4, 5, 6, 8, 9)] == [500, 500, 500, 500, 500, 500, 400]
+    # and through the Flask micro-batcher: a request that still raises inside the batch (an engine
+    # double that fails on one text) only fails itself
+    svc = make()
+    real = svc._run
+
+    def flaky(texts, *a):
+        if b"boom" in texts:
+            raise RuntimeError("unforeseen")
+        return real(texts, *a)
+    svc._run = flaky
+    A = pkg("app")
+    mb = A.MicroBatcher(svc, max_wait_s=0.05)
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(4) as ex:
+        futs = [ex.submit(mb.submit, k, d) for k, d in
+                [good[2], ("customer", {"conversation_id": "z", "transcript": "boom"}), good[0]]]
+        res = []
+        for f in futs:
+            try:
+                res.append(f.result())
+            except RuntimeError:
+                res.append("raised")
+    mb.close()
+    assert res[1] == "raised" and res[0][1] == 200 and res[2][1] == 200
+
+
 @pytest.mark.gpu
 def test_flask_concurrent_requests_on_gpu(oracle_cfg):
     """The Flask shim on the real engine: 8 client threads replay the golden transcripts' handler
