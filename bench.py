@@ -342,13 +342,16 @@ def main():
     ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5", "ner"], default="scan",
+    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5", "ner", "ner-redact"],
+                    default="scan",
                     help="scan = config 2 (headline); window = config 3 multi-turn re-scan; "
                          "stream = config 4 PCIe-inclusive batch stream; long = config-2 bytes as long rows; "
-                         "config5 = 500+ custom regex / dictionary infoTypes")
+                         "config5 = 500+ custom regex / dictionary infoTypes; ner = the BERT forward alone; "
+                         "ner-redact = NER detector + scan+redact with its PERSON_NAME spans in one step")
     ap.add_argument("--row-kb", type=int, default=1024, help="(long) row size, KiB")
     ap.add_argument("--ner-batch", type=int, default=64, help="(ner) sequences per step")
     ap.add_argument("--ner-seq", type=int, default=128, help="(ner) tokens per sequence")
+    ap.add_argument("--ner-rows", type=int, default=8192, help="(ner-redact) utterances per step")
     ap.add_argument("--window-n", type=int, default=5)
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
     ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
@@ -362,6 +365,8 @@ def main():
         return config5_main(args)
     if args.workload == "ner":
         return ner_main(args)
+    if args.workload == "ner-redact":
+        return ner_redact_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
 
@@ -469,6 +474,133 @@ def ner_main(args):
                      "algorithmic_flop": int(g_flop), "launch_ms": round(g_ms / 4, 4)},
         "cpu_baseline": cpu,
     }
+    print(json.dumps(line), flush=True)
+
+
+def _name_rows(n_rows, seed=synth.SEED):
+    """config-2-shaped conversations (16 utterances each, AGENT / END_USER alternating) whose customer
+    rows say a name half of the time ("my name is Jane Kim. ...")"""
+    import random
+    r = random.Random(seed)
+    bank = synth.build_bank(4096, 4096, seed=seed)
+    texts, roles, convs = [], [], []
+    for i in range(n_rows):
+        agent = i % 2 == 0
+        t = r.choice(bank.texts[:4096] if agent else bank.texts[4096:])
+        if not agent and r.random() < 0.5:
+            t = f"my name is {r.choice(synth.NAMES).capitalize()} {r.choice(synth.NAMES).capitalize()}. ".encode() + t
+        texts.append(t)
+        roles.append(1 if agent else 0)
+        convs.append(i // 16)
+    return texts, roles, convs
+
+
+def ner_redact_main(args):
+    """SURVEY §8(f)4 on the redaction path: one step = the NER detector on the GPU (k_tokenize ->
+    bf16 BERT-base forward on MFMA -> k_ner_spans) over --ner-rows resident utterances, then the
+    scan+redact call with its PERSON_NAME spans as external candidates (pii_scan_redact_device_ext),
+    no host round trip in between.  value = transcript MB/s of the whole step; the NER and engine
+    shares come from HIP events on the stream both run on.  cpu_baseline = HF fp32 NER + the oracle
+    on a sample of the same rows, on the host's CPU share."""
+    import torch
+    N = importlib.import_module("context-based-pii_amd.ner")
+    E = importlib.import_module("context-based-pii_amd.engine")
+    n, S = args.ner_rows, 64
+    texts, roles, convs = _name_rows(n)
+    data, offs = E.pack(texts)
+    ref = N.reference_model(seed=0)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import pii_oracle as O
+        cores = cpu_share()
+        torch.set_num_threads(cores)
+        cfg = O.RuleConfig.load()
+        P = cfg.type_id["PERSON_NAME"]
+        nb = min(n, 256)
+        tok = N.HashTokenizer(max_len=S)
+        t0 = time.perf_counter()
+        ids, mask, sp = tok.batch(texts[:nb])
+        with torch.no_grad():
+            lab = ref(input_ids=torch.as_tensor(ids, dtype=torch.long),
+                      attention_mask=torch.as_tensor(mask, dtype=torch.long)).logits.argmax(-1).numpy()
+        ext = [[(a, b, P, N.LIKELY) for a, b in N.decode_spans(lab[i], sp[i])] for i in range(nb)]
+        O.process_rows([(convs[i], roles[i], texts[i], 0) for i in range(nb)], cfg, extra=ext)
+        dt = time.perf_counter() - t0
+        nbytes = int(offs[nb])
+        cpu = {"value": round(nbytes / dt / 1e6, 4), "unit": "MB/s", "cores": cores, "kind": "port",
+               "host_cpu": host_cpu_model(),
+               "sample": f"{nb} of the step's utterances ({nbytes} B): HashTokenizer + HF BertForTokenClassification "
+                         f"fp32 (torch.set_num_threads({cores})) + oracle/pii_oracle.py process_rows with the spans, "
+                         f"wall {dt:.2f}s"}
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comp = compiler.compile_default()
+    eng = E.Engine(comp.blob, device=0, n_conv_slots=n // 16 + 2)
+    P = eng.type_names.index("PERSON_NAME")
+    m = N.BertNer(ref, device=0)
+    d_text = torch.from_numpy(np.concatenate([data, np.zeros(64, np.uint8)])).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_slot = torch.tensor(convs, dtype=torch.int32, device=dev)
+    d_role = torch.tensor(roles, dtype=torch.uint8, device=dev)
+    d_ts = torch.zeros(n, dtype=torch.int64, device=dev)
+    out_cap = int(offs[-1]) * 4 + 64 * n
+    span_cap = int(offs[-1]) + n
+    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
+    d_ctx = torch.empty(n, dtype=torch.int16, device=dev)
+    st = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    acc = np.zeros(2)
+
+    def step(timed):
+        eng.histogram_reset()
+        ev[0].record(st)
+        ext, ext_n, stride = m.detect_device(d_text.data_ptr(), d_offs.data_ptr(), n, S=S, info_type=P)
+        ev[1].record(st)
+        eng.scan_redact_device_ext(d_text.data_ptr(), d_offs.data_ptr(), n, 0, int(offs[-1]), d_slot.data_ptr(),
+                                   d_role.data_ptr(), d_ts.data_ptr(), d_out.data_ptr(), out_cap, d_oo.data_ptr(),
+                                   d_sp.data_ptr(), span_cap, d_ctx.data_ptr(), ext.data_ptr(), ext_n.data_ptr(),
+                                   stride, st.cuda_stream)
+        ev[2].record(st)
+        ob, ns, fl = eng.sync()
+        if fl:
+            raise RuntimeError(f"engine error flags {fl}")
+        if timed:
+            ev[2].synchronize()
+            acc[0] += ev[0].elapsed_time(ev[1])
+            acc[1] += ev[1].elapsed_time(ev[2])
+        return ns
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ns = step(True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    hist = eng.histogram()
+    tokens = n * S
+    flop = m.flops_per_token(S) * tokens
+    ner_ms, eng_ms = acc / args.steps
+    line = {
+        "metric": "config 5 NER on the redaction path: transcript MB/s (NER + scan+redact per step)",
+        "value": round(int(offs[-1]) * args.steps / el / 1e6, 3), "unit": "MB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"{n} config-2 utterances (16 per conversation, half the customer rows with a name), "
+                               f"NER at {S} tokens per utterance (BertConfig() seeded random weights) -> PERSON_NAME "
+                               f"external candidates -> scan+redact with context", "bytes_per_step": int(offs[-1])},
+        "utt_per_s": round(n * args.steps / el, 1),
+        "ner_ms": round(float(ner_ms), 3), "engine_ms": round(float(eng_ms), 3),
+        "ner_tflops": round(flop / (ner_ms / 1e3) / 1e12, 1),
+        "person_name_findings_last_step": int(hist[P]), "spans_last_step": int(ns),
+        "roofline": {"bound": "mfma", "kernel": "NER forward (k_gemm + attention)", "achieved":
+                     round(flop / (ner_ms / 1e3) / 1e12, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(flop / (ner_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None},
+        "cpu_baseline": cpu,
+    }
+    eng.close()
     print(json.dumps(line), flush=True)
 
 

@@ -31,6 +31,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {      // round to nearest eve
 }
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
+constexpr int32_t CLS_ID = 101, SEP_ID = 102, PAD_ID = 0;     // (ner.py CLS, SEP, PAD)
 constexpr int G_THREADS = 256;
 
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2 };
@@ -405,9 +406,145 @@ __global__ __launch_bounds__(256) void k_classify(const uint16_t* __restrict__ h
     }
 }
 
+// ------------------------------------------------------------------ detector front and back end
+// ner.py HashTokenizer.encode on the device, one thread per row: tokens are maximal [A-Za-z0-9_]+
+// runs or single bytes that are neither word bytes nor whitespace (Python bytes-regex \s = " \t\n
+// \v\f\r"), ASCII lower-cased, id = 1000 + fnv1a64(token) % (vocab - 1000); a row is [CLS] tokens
+// [SEP] [PAD]..., at most S ids.  Token byte ranges (row relative) go to tok_lo / tok_hi.
+__device__ __forceinline__ bool ner_word(uint32_t c) {
+    return (c - 48u < 10u) || ((c | 32u) - 97u < 26u) || c == 95u;
+}
+__device__ __forceinline__ bool ner_space(uint32_t c) { return c == 32u || (c - 9u < 5u); }
+
+__global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ text, const uint64_t* __restrict__ offs,
+                                                  int n_rows, int S, int vocab, int32_t* __restrict__ ids,
+                                                  int32_t* __restrict__ mask, uint32_t* __restrict__ tok_lo,
+                                                  uint32_t* __restrict__ tok_hi, int32_t* __restrict__ n_tok) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    const uint64_t b = offs[r], len = offs[r + 1] - b;
+    const uint8_t* t = text + b;
+    const size_t o = (size_t)r * S;
+    int k = 0;
+    ids[o] = CLS_ID;
+    tok_lo[o] = tok_hi[o] = 0;
+    ++k;
+    uint64_t i = 0;
+    while (i < len && k < S - 1) {
+        const uint32_t c = t[i];
+        if (ner_space(c)) {
+            ++i;
+            continue;
+        }
+        uint64_t h = 0xcbf29ce484222325ull;
+        const uint64_t s0 = i;
+        if (ner_word(c)) {
+            while (i < len && ner_word(t[i])) {
+                const uint32_t x = t[i] - 65u < 26u ? t[i] + 32u : t[i];
+                h = (h ^ x) * 0x100000001b3ull;
+                ++i;
+            }
+        } else {
+            h = (h ^ c) * 0x100000001b3ull;     // (not a letter: lower() leaves it)
+            ++i;
+        }
+        ids[o + k] = 1000 + (int32_t)(h % (uint64_t)(vocab - 1000));
+        tok_lo[o + k] = (uint32_t)s0;
+        tok_hi[o + k] = (uint32_t)i;
+        ++k;
+    }
+    ids[o + k] = SEP_ID;
+    tok_lo[o + k] = tok_hi[o + k] = 0;
+    ++k;
+    n_tok[r] = k;
+    for (int j = 0; j < S; ++j) mask[o + j] = j < k ? 1 : 0;
+    for (int j = k; j < S; ++j) {
+        ids[o + j] = PAD_ID;
+        tok_lo[o + j] = tok_hi[o + j] = 0;
+    }
+}
+
+// ner.py decode_spans on the device, one thread per row: argmax label per token (first maximum, as
+// torch.argmax), BIO-merged into PERSON_NAME byte spans, written as the engine's external candidates
+// (include/pii_engine.h pii_scan_redact_device_ext): ext[r * S + j], ext_n[r].
+struct ExtSpan {      // = pii_span (16 B)
+    uint32_t utt, start, end;
+    uint16_t info_type;
+    uint8_t likelihood, flags;
+};
+__global__ __launch_bounds__(256) void k_ner_spans(const float* __restrict__ logits, int L,
+                                                   const uint32_t* __restrict__ tok_lo,
+                                                   const uint32_t* __restrict__ tok_hi,
+                                                   const int32_t* __restrict__ n_tok, int n_rows, int S,
+                                                   int info_type, int likelihood, ExtSpan* __restrict__ ext,
+                                                   uint32_t* __restrict__ ext_n) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    const size_t o = (size_t)r * S;
+    const int nt = n_tok[r];
+    uint32_t n = 0;
+    int cs = -1, ce = -1;
+    auto flush = [&]() {
+        if (cs >= 0) {
+            ExtSpan x;
+            x.utt = (uint32_t)r;
+            x.start = (uint32_t)cs;
+            x.end = (uint32_t)ce;
+            x.info_type = (uint16_t)info_type;
+            x.likelihood = (uint8_t)likelihood;
+            x.flags = 0;
+            ext[o + n++] = x;
+        }
+        cs = -1;
+    };
+    for (int j = 0; j < nt; ++j) {
+        const float* lg = logits + (o + j) * L;
+        int lab = 0;
+        float best = lg[0];
+        for (int c = 1; c < L; ++c)
+            if (lg[c] > best) {
+                best = lg[c];
+                lab = c;
+            }
+        const int s = (int)tok_lo[o + j], e = (int)tok_hi[o + j];
+        if (e <= s) {                      // [CLS] / [SEP]
+            flush();
+        } else if (lab == 1 || (lab == 2 && cs < 0)) {
+            flush();
+            cs = s;
+            ce = e;
+        } else if (lab == 2) {
+            ce = e;
+        } else {
+            flush();
+        }
+    }
+    flush();
+    ext_n[r] = n;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ner_tokenize(const uint8_t* text, const uint64_t* offs, int n_rows, int S, int vocab, int32_t* ids, int32_t* mask,
+                 uint32_t* tok_lo, uint32_t* tok_hi, int32_t* n_tok, void* stream) {
+    if (!text || !offs || !ids || !mask || !tok_lo || !tok_hi || !n_tok || n_rows <= 0 || S < 2 || vocab <= 1000)
+        return -1;
+    k_tokenize<<<(n_rows + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(text, offs, n_rows, S, vocab, ids,
+                                                                                  mask, tok_lo, tok_hi, n_tok);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int ner_spans(const float* logits, int L, const uint32_t* tok_lo, const uint32_t* tok_hi, const int32_t* n_tok,
+              int n_rows, int S, int info_type, int likelihood, void* ext, uint32_t* ext_n, void* stream) {
+    if (!logits || !tok_lo || !tok_hi || !n_tok || !ext || !ext_n || n_rows <= 0 || L < 3 || S < 2 ||
+        likelihood < 1 || likelihood > 5 || info_type < 0 || info_type > 0xffff)
+        return -1;
+    k_ner_spans<<<(n_rows + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+        logits, L, tok_lo, tok_hi, n_tok, n_rows, S, info_type, likelihood, static_cast<ExtSpan*>(ext), ext_n);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 int ner_gemm(const void* A, const void* W, const void* bias, const void* resid, void* C, int M, int N, int K,
              int epi, void* stream) {

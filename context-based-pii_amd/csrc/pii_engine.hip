@@ -1907,8 +1907,11 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
         }
         best_e = -1;
     };
+    // a whole row's output length, written (not added: k_sel_fix re-runs whole lanes, and a re-run
+    // must not count the whole rows of its lanes twice); rows without findings keep the length
+    // k_chunk_index wrote
     auto flush_utt = [&]() {
-        if (nf_u) io.out_len[u] += (uint32_t)delta_u;      // (k_chunk_index wrote the row length)
+        if (nf_u) io.out_len[u] = (uint32_t)(g_off(g, u + 1) - g_off(g, u)) + (uint32_t)delta_u;
     };
     // candidate (row pu, start ps, end e) enters: row / start transitions
     auto enter = [&](uint32_t pu, int ps, int e) {

@@ -26,6 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 NER_LIB = os.environ.get("PII_NER_LIB") or os.path.join(HERE, "libner.so")
 LABELS = ["O", "B-PERSON_NAME", "I-PERSON_NAME"]
 EPI_BIAS, EPI_GELU, EPI_RESID = 0, 1, 2
+LIKELY = 4                  # likelihood of a PERSON_NAME finding (DLP scale)
 CLS, SEP, PAD = 101, 102, 0
 
 _LIB = None
@@ -45,7 +46,9 @@ def load_library(path: str = NER_LIB) -> ctypes.CDLL:
     lib.ner_embed.argtypes = [P, P, P, P, P, P, P, I, I, I, F, P]
     lib.ner_attention.argtypes = [P, P, P, I, I, I, I, P]
     lib.ner_classify.argtypes = [P, P, P, P, I, I, I, P]
-    for n in ("ner_gemm", "ner_layernorm", "ner_embed", "ner_attention", "ner_classify"):
+    lib.ner_tokenize.argtypes = [P, P, I, I, I, P, P, P, P, P, P]
+    lib.ner_spans.argtypes = [P, I, P, P, P, I, I, I, I, P, P, P]
+    for n in ("ner_gemm", "ner_layernorm", "ner_embed", "ner_attention", "ner_classify", "ner_tokenize", "ner_spans"):
         getattr(lib, n).restype = ctypes.c_int
     _LIB = lib
     return lib
@@ -142,6 +145,7 @@ class BertNer:
         if cfg.hidden_size // cfg.num_attention_heads != 64 or cfg.hidden_act != "gelu":
             raise ValueError("the GPU kernels implement head size 64 and exact GELU (BertConfig defaults)")
         self.H, self.heads, self.L = cfg.hidden_size, cfg.num_attention_heads, cfg.num_labels
+        self.vocab = cfg.vocab_size
         self.eps = float(cfg.layer_norm_eps)
         self.dev = torch.device("cuda", device)
         sd = {k: v.detach().float() for k, v in model.state_dict().items()}
@@ -208,6 +212,13 @@ class BertNer:
         Mp = (M + 127) // 128 * 128
         bu = self._buffers(Mp)
         bu["ids"][:M] = ids.reshape(-1)
+        # a copy: the buffer is reused by the next forward of the same padded size
+        return self._forward_ids(bu, mask, B, S).reshape(B, S, self.L).clone()
+
+    def _forward_ids(self, bu, mask, B, S):
+        """the 12-layer forward over bu["ids"][:B*S] -> logits [B*S, L] (a view of the buffer)"""
+        M = B * S
+        Mp = bu["h"].shape[0]
         st = self._st()
         h, h1, a, ctx, qkv, f = bu["h"], bu["h1"], bu["a"], bu["ctx"], bu["qkv"], bu["f"]
         self._check(self.lib.ner_embed(bu["ids"].data_ptr(), self.wemb.data_ptr(), self.pemb.data_ptr(),
@@ -224,7 +235,7 @@ class BertNer:
             self.layernorm(a, Ly["g2"], Ly["b2"], h)
         self._check(self.lib.ner_classify(h.data_ptr(), self.wc.data_ptr(), self.bc.data_ptr(),
                                           bu["logits"].data_ptr(), Mp, self.H, self.L, st), "ner_classify")
-        return bu["logits"][:M].reshape(B, S, self.L)
+        return bu["logits"][:M]
 
     def flops_per_token(self, S: int) -> float:
         H, I = self.H, self.inter
@@ -239,3 +250,40 @@ class BertNer:
         ids, mask, spans = tok.batch(texts)
         lab = self.forward(ids, mask).argmax(-1).cpu().numpy()
         return [decode_spans(lab[i], spans[i]) for i in range(len(texts))]
+
+    def detect_device(self, d_text, d_offs, n_rows: int, S: int = 64, info_type: int = 0,
+                      likelihood: int = LIKELY):
+        """The whole detector on the GPU, for rows already in HBM (d_text / d_offs: device pointers of
+        the engine's batch layout, offsets relative to d_text): tokenize (k_tokenize = HashTokenizer
+        with max_len S) -> bf16 BERT forward -> argmax + BIO decode (k_ner_spans = decode_spans) ->
+        the engine's external candidates.  Returns (ext, ext_n, stride) device tensors for
+        Engine.scan_redact_device_ext; nothing is copied to the host.  Rows past S - 2 tokens are
+        truncated, as HashTokenizer does."""
+        t = self.torch
+        if S % 32 or S > 128:
+            raise ValueError("S must be a multiple of 32, at most 128 (the matrix-core attention)")
+        st = self._st()
+        M = n_rows * S
+        Mp = (M + 127) // 128 * 128
+        bu = self._buffers(Mp)
+        i32 = dict(dtype=t.int32, device=self.dev)
+        mask = t.empty(M, **i32)
+        lo = t.empty(M, dtype=t.int32, device=self.dev)
+        hi = t.empty(M, dtype=t.int32, device=self.dev)
+        ntok = t.empty(n_rows, **i32)
+        self._check(self.lib.ner_tokenize(d_text, d_offs, n_rows, S, self.vocab, bu["ids"].data_ptr(),
+                                          mask.data_ptr(), lo.data_ptr(), hi.data_ptr(), ntok.data_ptr(), st),
+                    "ner_tokenize")
+        logits = self._forward_ids(bu, mask.view(n_rows, S), n_rows, S)
+        ext = t.empty((n_rows * S, 4), dtype=t.int32, device=self.dev)      # pii_span rows (16 B)
+        ext_n = t.empty(n_rows, **i32)
+        self._check(self.lib.ner_spans(logits.data_ptr(), self.L, lo.data_ptr(), hi.data_ptr(), ntok.data_ptr(),
+                                       n_rows, S, info_type, likelihood, ext.data_ptr(), ext_n.data_ptr(), st),
+                    "ner_spans")
+        return ext, ext_n, S
+
+    def ext_candidates(self, texts: Sequence[bytes], info_type: int, likelihood: int = LIKELY,
+                       max_len: int = 64):
+        """Host form for Engine.scan_redact(..., ext=): per text [(start, end, info_type, likelihood)]"""
+        return [[(s, e, info_type, likelihood) for s, e in sp]
+                for sp in self.detect(texts, HashTokenizer(self.vocab, max_len))]

@@ -145,7 +145,7 @@ class PiiService:
 
     def __init__(self, engine: Optional[Engine] = None, n_slots: int = 1 << 16,
                  ttl_seconds: int = CONTEXT_TTL_SECONDS, clock: Callable[[], float] = time.time, device: int = 0,
-                 time_base: str = "wall"):
+                 time_base: str = "wall", ner=None, ner_max_len: int = 64):
         if time_base not in ("wall", "payload"):
             raise ValueError("time_base must be 'wall' or 'payload'")
         self.engine = engine if engine is not None else Engine.from_rules(device=device, n_conv_slots=n_slots,
@@ -160,6 +160,14 @@ class PiiService:
         for g, t in enumerate(self.engine.group_types):
             self.group_of_type.setdefault(t, g)
         self.agent_text: Dict[int, Tuple[str, int]] = {}     # slot -> (agent transcript, ts_us)
+        # optional NER detector (ner.BertNer): its PERSON_NAME spans join every engine call's overlap
+        # resolution as external candidates (pii_scan_redact_ext), so they are redacted like any finding
+        self.ner = ner
+        self.ner_max_len = ner_max_len
+        if ner is not None:
+            if "PERSON_NAME" not in self.engine.type_names:
+                raise ValueError("the rules have no PERSON_NAME type (builtin_infotypes.yaml external_types)")
+            self.ner_type = self.engine.type_names.index("PERSON_NAME")
 
     # ---------------------------------------------------------------- helpers
     def _now_us(self) -> int:
@@ -193,7 +201,10 @@ class PiiService:
         return rec
 
     def _run(self, texts: Sequence[bytes], slots: Sequence[int], roles: Sequence[int], ts: Sequence[int]):
-        return self.engine.scan_redact(texts, slots, roles, ts)
+        if self.ner is None:
+            return self.engine.scan_redact(texts, slots, roles, ts)
+        ext = self.ner.ext_candidates(texts, self.ner_type, max_len=self.ner_max_len)
+        return self.engine.scan_redact(texts, slots, roles, ts, ext=ext)
 
     def _sub_batches(self, keys: Sequence[object], split_before: Optional[Sequence[bool]] = None) -> List[List[int]]:
         """Row indices cut into runs whose distinct-conversation count fits the slot table (so

@@ -159,3 +159,59 @@ def test_thousand_1mb_rows_split_property(eng):
     rows_per = 4000
     assert len(utts) // rows_per == 1000
     _split_property(eng, utts, rows_per)
+
+
+def test_whole_rows_before_and_after_a_long_row(eng, oracle_cfg):
+    """k_sel_fix re-runs the clean lane that holds a cut row's start (and the dirty lanes after it)
+    when a match of the cut row reaches over a cut: the whole rows sharing those lanes must keep
+    their output lengths (counted once).  Short rows with findings packed around long rows whose
+    matches straddle the first cut, at 128-byte lanes (a small batch) and at 1 KiB lanes."""
+    from oracle import pii_oracle as O
+    synth = pkg("synth")
+    r = random.Random(17)
+    bank = synth.build_bank(300, 300, seed=17)
+    for n_pad in (0, 700_000):
+        rows = []
+        for k in range(120):
+            rows.append((k, O.ROLE_CUSTOMER, b"mail me at jo@ex.com ok", 0))
+            email = ("".join(r.choice("abcxyz0123._") for _ in range(r.randrange(20, 300))) + "@example.com").encode()
+            lead = b"y" * r.randrange(0, 200)
+            rows.append((k, O.ROLE_CUSTOMER, lead + b" " + email + b" " + r.choice(bank.texts) * r.randrange(3, 30), 0))
+            rows.append((k, O.ROLE_CUSTOMER, r.choice(bank.texts[300:]), 0))
+        n_head = len(rows)
+        if n_pad:                                  # a big batch (> 64 MB): 1 KiB lanes
+            rows += [(121 + i % 3000, O.ROLE_CUSTOMER, bank.texts[i % len(bank.texts)], 0) for i in range(n_pad)]
+            rows.sort(key=lambda x: x[0])
+        res = eng.scan_redact([t for _, _, t, _ in rows], [c + 1 for c, _, _, _ in rows], [x for _, x, _, _ in rows],
+                              [0] * len(rows))
+        if n_pad:
+            assert eng.stats()["lane_bytes"] == 1024
+        exp = O.process_rows(rows[:n_head], oracle_cfg)          # the conversations with the long rows
+        for i, (red, fs, _, _) in enumerate(exp):
+            assert res.text(i) == red, (n_pad, i)
+            assert _spans(res, i) == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], (n_pad, i)
+
+
+def test_2mb_row_of_joined_utterances_vs_oracle(eng, oracle_cfg):
+    """A 2 MB row of synthetic utterances joined by '\\n' / ' ' (the aggregator's joins and the
+    realtime join, README.md:131-134, main_service/main.py:457): hotwords of one utterance reach the
+    PII of the next across the joins and across 2000 lane cuts; the row is redacted with a context
+    (the agent row's SSN request) and without."""
+    from oracle import pii_oracle as O
+    synth = pkg("synth")
+    r = random.Random(23)
+    bank = synth.build_bank(2000, 2000, seed=23)
+    parts, n = [], 0
+    while n < 2_100_000:
+        p = r.choice(bank.texts)
+        parts += [p, r.choice([b"\n", b" "])]
+        n += len(p) + 1
+    text = b"".join(parts)
+    rows = [(1, O.ROLE_AGENT, b"Could you confirm your social security number please?", 0),
+            (1, O.ROLE_CUSTOMER, text, 1), (2, O.ROLE_OTHER, text, 2)]
+    res = eng.scan_redact([t for _, _, t, _ in rows], [5, 5, 6], [x for _, x, _, _ in rows], [0, 1, 2])
+    exp = O.process_rows(rows, oracle_cfg)
+    for i, (red, fs, _, _) in enumerate(exp):
+        assert res.text(i) == red, i
+        assert _spans(res, i) == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], i
+    assert len(exp[1][1]) > 1000 and exp[1][2] == "US_SOCIAL_SECURITY_NUMBER"     # the context was applied
