@@ -3633,6 +3633,52 @@ __global__ __launch_bounds__(256) void k_win_commit(const WinRing W, const WinBa
     }
 }
 
+// ---- full re-scan of the joined windows (rule sets the incremental path cannot take: a detector that
+// consumes '\n' or tests a text edge, several SCAN groups, tables past LDS).  The ring then holds the
+// raw text only (no resident candidates, wc_n = 0); each row's window "\n".join(ring entries, batch
+// predecessors, row) is materialised in HBM and run through the ordinary pipeline as one row.
+// per row: its joined window's length
+__global__ __launch_bounds__(256) void k_win_jlen(const WinRing W, const WinBatch B, uint32_t* __restrict__ jlen,
+                                                  const uint32_t* __restrict__ err) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= B.n_utt) return;
+    if (*err & (ERR_ABORT | ERR_SLOT)) {
+        jlen[u] = 0;
+        return;
+    }
+    const WinIt it = win_begin(W, B, u);
+    uint32_t n = (uint32_t)it.nw - 1u;
+    for (int j = 0; j < it.nw; ++j) n += win_at(W, B, it, j).len;
+    jlen[u] = n;
+}
+
+// one wavefront per row: copy its window's entries and the '\n' joins to jbuf + joff[u]
+__global__ __launch_bounds__(256) void k_win_join(const WinRing W, const WinBatch B, const uint64_t* __restrict__ joff,
+                                                  uint8_t* __restrict__ jbuf, const uint32_t* __restrict__ err) {
+    const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (u >= B.n_utt || (*err & (ERR_ABORT | ERR_SLOT))) return;
+    const WinIt it = win_begin(W, B, u);
+    uint64_t pos = joff[u];
+    for (int j = 0; j < it.nw; ++j) {
+        const WEntry E = win_at(W, B, it, j);
+        for (uint32_t k = lane; k < E.len; k += 64) jbuf[pos + k] = E.t[k];
+        pos += E.len;
+        if (j + 1 < it.nw) {
+            if (lane == 0) jbuf[pos] = '\n';
+            ++pos;
+        }
+    }
+}
+
+// the counter block a second pass over the same call starts from: the first pass's error flags
+// (minus a queue overflow of its pair queue, whose pairs are not used) and its context commit count
+__global__ void k_err_save(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ saved) {
+    saved[0] = cnt[0] & ~(uint32_t)ERR_QUEUE;
+    saved[1] = 0;
+    saved[2] = cnt[2];
+    saved[3] = saved[4] = saved[5] = 0;
+}
+
 __global__ void k_noop() {}
 
 // ------------------------------------------------------------------------------- LDS images
@@ -3853,6 +3899,18 @@ struct pii_engine {
     uint32_t wcap_utt = 0;
     pii_span* wfd = nullptr;
     uint64_t wfd_cap = 0;
+    // full window re-scan (win_full): joined windows, their offsets, a second keyword array, all-CUSTOMER
+    // roles and the first pass's counter block
+    bool win_full = false;
+    uint8_t* jbuf = nullptr;
+    uint64_t cap_jbuf = 0;
+    uint64_t* joff = nullptr;
+    uint32_t* jlen = nullptr;
+    int32_t* kw2 = nullptr;
+    uint8_t* jrole = nullptr;
+    uint32_t cap_j_utt = 0;
+    uint32_t* err_saved = nullptr;
+    uint64_t* h_jtotal = nullptr;      // pinned: the joined bytes of the call
     // lane-based resolve, long rows, span-driven redaction
     uint32_t r0 = 0, long_min = NO_CUTS;
     uint32_t* long_rows = nullptr;     // rows cut into several lanes (k_chunk_index)
@@ -4086,13 +4144,17 @@ size_t hist_bytes(const pii_engine* e) { return 64 + (size_t)std::max(e->R.T, 25
 // pattern) pair queue, context (segmented scan), leftmost-first confirmation.  Records tev[0..2].
 int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint32_t n_chunks,
                  uint64_t base, uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts,
-                 int16_t* ctx, int16_t* win_ctx, const unsigned long long* pcount, hipStream_t st) {
+                 int16_t* ctx, int16_t* win_ctx, const unsigned long long* pcount, hipStream_t st,
+                 const uint32_t* err_init = nullptr, bool ctx_kernels = true, bool pair_first = true) {
     const RulesDev& R = e->R;
     if (e->reset_pending && st != e->stream) HIPCHK(hipStreamSynchronize(e->stream));   // order the reset
     e->reset_pending = false;
     e->epoch += 1;
     const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
-    HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));       // err, long_count, ncommit, pair_count
+    if (err_init)              // a second pass over the call: start from the first pass's counter block
+        HIPCHK(hipMemcpyAsync(e->d_err, err_init, 24, hipMemcpyDeviceToDevice, st));
+    else
+        HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));   // err, long_count, ncommit, pair_count
     HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt / CI_ROWS + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
@@ -4154,7 +4216,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     }
     HIPCHK(hipEventRecord(e->tev[1], st));
     const uint32_t nblk = (uint32_t)(((uint64_t)n_utt + CTX_TILE - 1) / CTX_TILE);
-    if (n_utt > 0) {
+    if (n_utt > 0 && ctx_kernels) {
         // 16-byte row groups when the caller's arrays allow it
         const bool vec = ((uintptr_t)slot & 15) == 0 && ((uintptr_t)role & 7) == 0 && ((uintptr_t)ts & 15) == 0 &&
                          ((uintptr_t)ctx & 15) == 0 && ((uintptr_t)win_ctx & 15) == 0;
@@ -4166,7 +4228,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[2], st));
-    if (n_utt > 0 && n_chunks > 0) {
+    if (n_utt > 0 && n_chunks > 0 && pair_first) {
         (e->img_first.global ? k_pair_first<true> : k_pair_first<false>)<<<e->n_seg, PAIR_BLOCK,
                                                                             e->img_first.lds(), st>>>(
             e->img_first.d, e->img_first.li, text, offs, pcount, e->pair_cap, e->evloc, e->pres, e->pend, e->matched,
@@ -4176,11 +4238,26 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     return PII_OK;
 }
 
+// The second pass of a full window re-scan (run_window_full): the joined windows as rows, each with the
+// context group its window uses (no context kernels), the first pass's counter block, and the commits
+// of the NEW rows (ring entries, context records) after a successful redaction.
+struct WinFull {
+    const int16_t* ctx_given;
+    const uint32_t* err_init;
+    WinRing W;
+    WinBatch Bnew;
+    const WNew* wnew;
+    const uint32_t* slot_new;
+    const int64_t* ts_new;
+    const int32_t* kw_new;
+    uint32_t n_new;
+};
+
 int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
                  uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out,
                  uint64_t out_cap, uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* ctx_info,
                  hipStream_t st, const pii_span* ext = nullptr, const uint32_t* ext_n = nullptr,
-                 uint32_t ext_stride = 0) {
+                 uint32_t ext_stride = 0, const WinFull* wf = nullptr) {
     if (total_bytes > PII_MAX_BATCH_BYTES || total_bytes + 2ull * n_utt + (total_bytes >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
         return PII_E_ARG;
@@ -4200,18 +4277,20 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     if (has_ext) Rsel.min_len = 1;
     int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks, Rsel.min_len);
     if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_redact(e, span_cap, out_cap))) return rc;
-    e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
-                               span_cap, ctx_info, st, ext, ext_n, ext_stride};
-    e->last_kind = 0;
+    if (!wf) {                  // (a window call keeps its own record for pii_sync's re-run)
+        e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
+                                   span_cap, ctx_info, st, ext, ext_n, ext_stride};
+        e->last_kind = 0;
+    }
     const RulesDev& R = e->R;
-    int16_t* ctx = ctx_info ? ctx_info : e->ctx;
+    int16_t* ctx = wf ? const_cast<int16_t*>(wf->ctx_given) : ctx_info ? ctx_info : e->ctx;
     e->kev_valid = n_utt > 0 && total_bytes > 0;
     const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
     // queue length = the lane-count scan's total (lane_pair[n_chunks]); 0 for an empty batch
     const unsigned long long* pcount =
         n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
     if ((rc = launch_front(e, text, offs, n_utt, n_chunks, base, total_bytes, slot, role, ts, ctx, nullptr, pcount,
-                           st)))
+                           st, wf ? wf->err_init : nullptr, wf == nullptr)))
         return rc;
     if (n_utt > 0 && n_chunks > 0) {
         (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
@@ -4254,11 +4333,19 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_redact<<<tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
                                                      total_bytes, e->tile_first, e->d_err, out);
             HIPCHK(hipEventRecord(e->kev[3], st));
-            k_hist_reduce<<<dim3(e->hist_types, std::max(1u, std::min(32u, nsb / 256))), 256, 0, st>>>(
-                e->hist_part, nsb, (int)e->hist_types, e->d_err, e->hist);
+            if (!wf)        // (window findings are not counted, as on the incremental window path)
+                k_hist_reduce<<<dim3(e->hist_types, std::max(1u, std::min(32u, nsb / 256))), 256, 0, st>>>(
+                    e->hist_part, nsb, (int)e->hist_types, e->d_err, e->hist);
         }
-        k_ctx_commit<<<std::min<uint32_t>((n_utt + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
-            slot, e->kw, ts, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
+        if (wf) {           // the new rows enter their rings; their context records are written
+            k_win_commit<<<(uint32_t)(((uint64_t)wf->n_new * 16 + 255) / 256), 256, 0, st>>>(wf->W, wf->Bnew, wf->wnew,
+                                                                                             e->d_err);
+            k_ctx_commit<<<std::min<uint32_t>((wf->n_new + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
+                wf->slot_new, wf->kw_new, wf->ts_new, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
+        } else {
+            k_ctx_commit<<<std::min<uint32_t>((n_utt + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
+                slot, e->kw, ts, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
+        }
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[5], st));
@@ -4291,6 +4378,82 @@ int ensure_window_scratch(pii_engine* e, uint32_t n_utt) {
     return PII_OK;
 }
 
+int ensure_join(pii_engine* e, uint32_t n_utt) {
+    int rc;
+    if (n_utt + 1 > e->cap_j_utt) {
+        const uint32_t nu = std::max<uint32_t>(n_utt + n_utt / 8 + 2, 1024);
+        if ((rc = grow(e, e->jlen, nu)) || (rc = grow(e, e->joff, nu)) || (rc = grow(e, e->kw2, std::max(nu, e->cap_utt))) ||
+            (rc = grow(e, e->jrole, nu)))
+            return rc;
+        HIPCHK(hipMemset(e->jrole, PII_ROLE_CUSTOMER, nu));
+        e->cap_j_utt = nu;
+    }
+    if (!e->err_saved && (rc = grow(e, e->err_saved, 8))) return rc;
+    if (!e->h_jtotal) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&e->h_jtotal), 8));
+    return PII_OK;
+}
+
+// The full window re-scan (rule sets the incremental path cannot take, see k_win_jlen): pass 1 runs
+// the shared front over the NEW rows for their keyword groups and the context every window uses
+// (win_ctx), plans the ring commits (text only) and measures the joined windows; one host wait reads
+// the joined size; the windows are materialised; pass 2 is the ordinary pipeline over them as
+// CUSTOMER rows with the given context groups, then the new rows enter their rings and the context
+// records are written -- only when every stage succeeded.
+int run_window_full(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
+                    uint64_t total_bytes, const uint32_t* slot, const uint8_t* role, const int64_t* ts, uint8_t* out,
+                    uint64_t out_cap, uint64_t* out_offs, pii_span* spans, uint32_t span_cap, int16_t* win_ctx,
+                    hipStream_t st) {
+    e->lane_shift = pick_lane_shift(e, total_bytes);
+    e->r0 = (uint32_t)(((uintptr_t)text + base) & 63);
+    e->long_min = 2u << e->lane_shift;
+    const uint32_t n_chunks = lane_count(e, total_bytes);
+    e->last_lanes = n_chunks;
+    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
+    if (rc || (rc = ensure_queues(e, total_bytes)) || (rc = ensure_window_scratch(e, n_utt)) || (rc = ensure_join(e, n_utt)))
+        return rc;
+    e->last = pii_engine::Call{text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
+                               span_cap, win_ctx, st, nullptr, nullptr, 0};
+    e->last_kind = 1;
+    int16_t* wctx = win_ctx ? win_ctx : e->wctx;
+    const unsigned long long* pcount =
+        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, base, total_bytes, slot, role, ts, e->ctx, wctx, pcount, st,
+                           nullptr, true, false)))
+        return rc;
+    const WinRing W{e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->win_n, e->win_slot_bytes, e->n_slots, 0};
+    if (n_utt) HIPCHK(hipMemsetAsync(e->wc_n, 0, (size_t)n_utt * 4, st));      // text-only ring entries
+    const WinBatch B{text, offs, slot, e->wc, e->wc_first, e->wc_n, n_utt};
+    const uint32_t nb = (n_utt + 255) / 256;
+    if (n_utt) {
+        k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
+        k_win_alloc<<<nb, 256, 0, st>>>(W, B, e->wnew, e->d_err);
+        k_win_jlen<<<nb, 256, 0, st>>>(W, B, e->jlen, e->d_err);
+    }
+    k_err_save<<<1, 1, 0, st>>>(e->d_err, e->err_saved);
+    HIPCHK(hipGetLastError());
+    if ((rc = exclusive_scan(e, e->jlen, n_utt, e->joff, st))) return rc;
+    HIPCHK(hipMemcpyAsync(e->h_jtotal, e->joff + n_utt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t jt = *e->h_jtotal;
+    if (jt > PII_MAX_BATCH_BYTES || jt + 2ull * n_utt + (jt >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
+        e->err = "the call's joined windows exceed PII_MAX_BATCH_BYTES; split the batch";
+        return PII_E_ARG;
+    }
+    if (jt + 64 > e->cap_jbuf) {
+        if ((rc = grow(e, e->jbuf, jt + jt / 8 + 64))) return rc;
+        e->cap_jbuf = jt + jt / 8 + 64;
+    }
+    if (n_utt) k_win_join<<<(n_utt + 3) / 4, 256, 0, st>>>(W, B, e->joff, e->jbuf, e->d_err);
+    HIPCHK(hipGetLastError());
+    int32_t* kwA = e->kw;                // pass 2 must not overwrite the new rows' keyword groups
+    e->kw = e->kw2;
+    const WinFull wf{wctx, e->err_saved, W, B, e->wnew, slot, ts, kwA, n_utt};
+    rc = run_pipeline(e, e->jbuf, e->joff, n_utt, 0, jt, slot, e->jrole, ts, out, out_cap, out_offs, spans, span_cap,
+                      nullptr, st, nullptr, nullptr, 0, &wf);
+    e->kw = kwA;
+    return rc;
+}
+
 // the window re-scan call (a12): the shared front over the NEW rows only, then resident candidates,
 // window selection, window redaction, ring commit
 int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t base,
@@ -4304,6 +4467,9 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
         return PII_E_ARG;
     }
+    if (e->win_full)
+        return run_window_full(e, text, offs, n_utt, base, total_bytes, slot, role, ts, out, out_cap, out_offs, spans,
+                               span_cap, win_ctx, st);
     e->lane_shift = pick_lane_shift(e, total_bytes);
     e->r0 = (uint32_t)(((uintptr_t)text + base) & 63);
     e->long_min = NO_CUTS;                      // the window kernels keep rows whole
@@ -4814,10 +4980,12 @@ int pii_engine_destroy(pii_engine* e) {
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
                     e->long_rows, e->lane_st, e->lane_geo, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
-                    e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first, e->h_ext, e->h_ext_n};
+                    e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first, e->h_ext, e->h_ext_n, e->jbuf, e->joff,
+                    e->jlen, e->kw2, e->jrole, e->err_saved};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
+    if (e->h_jtotal) (void)hipHostFree(e->h_jtotal);
     for (auto& t : e->tev)
         if (t) (void)hipEventDestroy(t);
     for (auto& t : e->kev)
@@ -5136,17 +5304,14 @@ int pii_scan_redact_device_ext(pii_engine* e, const uint8_t* d_bytes, const uint
                        d_spans, span_cap, d_ctx_info, stream, decl, &x);
 }
 
-int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
-    if (!e || window_n == 0 || window_n > WN_MAX || slot_bytes < 64 || slot_bytes % 16) return PII_E_ARG;
-    if (!e->window_ok) {
-        e->err = "a detector can match '\\n' or a text edge: windows cannot be re-scanned incrementally";
-        return PII_E_RULES;
-    }
-    if (e->R.P > P_MAX || e->n_sg > 1 || !e->wsel_ok) {
-        e->err = "the window re-scan needs a rule set of at most P_MAX detector patterns, one SCAN group and "
-                 "LDS-resident tables";
-        return PII_E_RULES;
-    }
+int pii_window_enable_ex(pii_engine* e, uint32_t window_n, uint32_t slot_bytes, uint32_t flags) {
+    if (!e || window_n == 0 || window_n > WN_MAX || slot_bytes < 64 || slot_bytes % 16 ||
+        (flags & ~(uint32_t)PII_WINDOW_FULL))
+        return PII_E_ARG;
+    // the incremental path needs: no detector that consumes '\n' or tests a text edge (a match inside a
+    // window is then its utterance's own match), at most P_MAX patterns, one SCAN group, LDS-resident
+    // tables; any other rule set re-scans the joined windows in full
+    e->win_full = (flags & PII_WINDOW_FULL) || !e->window_ok || e->R.P > P_MAX || e->n_sg > 1 || !e->wsel_ok;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const size_t ns = std::max<uint32_t>(1, e->n_slots);
@@ -5159,6 +5324,15 @@ int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
     e->win_n = window_n;
     e->win_slot_bytes = slot_bytes;
     return PII_OK;
+}
+
+int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
+    return pii_window_enable_ex(e, window_n, slot_bytes, 0);
+}
+
+int pii_window_mode(pii_engine* e) {
+    if (!e || e->win_n == 0) return PII_E_ARG;
+    return e->win_full ? PII_WINDOW_FULL : 0;
 }
 
 int pii_window_reset(pii_engine* e, uint32_t slot) {

@@ -26,7 +26,9 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_context_set", "pii_histogram", "pii_histogram_reset", "pii_last_timings",
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
-           "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext"]
+           "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext", "pii_window_enable_ex",
+           "pii_window_mode"]
+PII_WINDOW_FULL = 1
 
 
 class PiiError(RuntimeError):
@@ -96,6 +98,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_last_queue_sizes.argtypes = [P, U64, U64]
     lib.pii_last_stats.argtypes = [P, U64, c.c_uint32]
     lib.pii_window_enable.argtypes = [P, c.c_uint32, c.c_uint32]
+    lib.pii_window_enable_ex.argtypes = [P, c.c_uint32, c.c_uint32, c.c_uint32]
+    lib.pii_window_mode.argtypes = [P]
     lib.pii_window_reset.argtypes = [P, c.c_uint32]
     lib.pii_window_count.argtypes = [P, c.c_uint32, U32]
     lib.pii_rescan_window.argtypes = lib.pii_scan_redact.argtypes
@@ -214,11 +218,19 @@ class Engine:
         n = max(1, self.window_n)
         return self._host_call(self.lib.pii_rescan_window, "pii_rescan_window", texts, conv_slot, role, ts_us, n)
 
-    def window_enable(self, window_n: int = 5, slot_bytes: int = 8192) -> None:
-        rc = self.lib.pii_window_enable(self.h, window_n, slot_bytes)
+    def window_enable(self, window_n: int = 5, slot_bytes: int = 8192, full: bool = False) -> None:
+        """full=True forces the full re-scan of the joined windows (rule sets the incremental path
+        cannot take get it anyway: window_mode() tells which one runs)"""
+        rc = self.lib.pii_window_enable_ex(self.h, window_n, slot_bytes, PII_WINDOW_FULL if full else 0)
         if rc != PII_OK:
-            raise self._err(rc, "pii_window_enable")
+            raise self._err(rc, "pii_window_enable_ex")
         self.window_n = window_n
+
+    def window_mode(self) -> str:
+        rc = self.lib.pii_window_mode(self.h)
+        if rc < 0:
+            raise self._err(rc, "pii_window_mode")
+        return "full" if rc == PII_WINDOW_FULL else "incremental"
 
     def window_reset(self, slot: int) -> None:
         rc = self.lib.pii_window_reset(self.h, slot)

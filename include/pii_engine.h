@@ -183,12 +183,20 @@ int pii_last_stats(struct pii_engine* e, uint64_t* out, uint32_t n);
  * re-scan scans only the NEW utterance; the rest of the window costs a hotword re-check where a
  * proximity window crosses a "\n", the context variant, and the output copy.  Output per row =
  * redact("\n".join(window ending at that row), current expected_pii_type) bit-exactly (SURVEY A.9,
- * oracle/pii_oracle.py window_rescan).  Needs rules where no detector can match '\n' or a text edge
- * (the shipped rules), else PII_E_RULES. */
+ * oracle/pii_oracle.py window_rescan), for every rule set: when no detector can match '\n' or a text
+ * edge and the rules fit one LDS-resident SCAN group (the shipped rules), incrementally; otherwise
+ * (config-5 scale rule sets, a '\n'-consuming detector) by a FULL re-scan -- the ring then keeps the
+ * raw text, every row's "\n"-joined window is materialised in HBM and run through the scan+redact
+ * pipeline (one host wait per call for the joined size). */
 #define PII_WINDOW_MAX 8
+#define PII_WINDOW_FULL 1   /* pii_window_enable_ex flag / pii_window_mode result: full re-scan */
 /* allocate the per-slot window history (n_conv_slots * slot_bytes of HBM); window_n <= PII_WINDOW_MAX,
  * slot_bytes a multiple of 16 (a window must fit: its utterances + 16 B per resident candidate) */
 int pii_window_enable(struct pii_engine* e, uint32_t window_n, uint32_t slot_bytes);
+/* the same; flags PII_WINDOW_FULL forces the full re-scan even for rules the incremental path takes */
+int pii_window_enable_ex(struct pii_engine* e, uint32_t window_n, uint32_t slot_bytes, uint32_t flags);
+/* PII_WINDOW_FULL or 0 (incremental) for an enabled window, else PII_E_ARG */
+int pii_window_mode(struct pii_engine* e);
 /* forget a conversation's window (the /conversation-ended endpoint, aggregator main.py) */
 int pii_window_reset(struct pii_engine* e, uint32_t slot);
 int pii_window_count(struct pii_engine* e, uint32_t slot, uint32_t* n_entries);

@@ -120,9 +120,44 @@ def test_config5_engine_vs_oracle(c5, c5_comp, c5_oracle):
         for f in fs:
             want[f.type_id] += 1
     assert (h.astype(np.int64) == want).all()
-    with pytest.raises(E.PiiError):
-        eng.window_enable(5, 8192)             # the window re-scan needs one SCAN group
     eng.close()
+
+
+@pytest.mark.gpu
+def test_config5_window_rescan(c5, c5_comp, c5_oracle):
+    """the aggregator re-scan with 500+ custom types (several SCAN groups: the full re-scan of the
+    joined windows) vs oracle.process_window_rows, one utterance per conversation per call"""
+    from oracle import pii_oracle as O
+    E = pkg("engine")
+    c, _ = c5
+    rows = _conversations(c, 120, 8, 13)
+    eng = E.Engine(c5_comp.blob, device=0, n_conv_slots=1 << 9)
+    try:
+        eng.window_enable(5, 16384)
+        assert eng.window_mode() == "full"
+        groups = list(c5_oracle.context_keywords.keys())
+        by_conv = {}
+        for row in rows:
+            by_conv.setdefault(row[0], []).append(row)
+        store, hist = O.ContextStore(), {}
+        n_custom = 0
+        for k in range(8):
+            batch = [by_conv[cv][k] for cv in sorted(by_conv) if k < len(by_conv[cv])]
+            res = eng.rescan_window([x[2] for x in batch], [x[0] for x in batch], [x[1] for x in batch],
+                                    [x[3] for x in batch])
+            exp = O.process_window_rows(batch, c5_oracle, n=5, store=store, history=hist)
+            for i, (red, fs, et) in enumerate(exp):
+                assert res.text(i) == red, (k, i)
+                m = res.spans["utt"] == i
+                got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"]))
+                       for s in res.spans[m]]
+                assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], (k, i)
+                g = int(res.ctx_info[i])
+                assert (groups[g] if g >= 0 else None) == et, (k, i)
+                n_custom += sum(c5_oracle.type_names[f.type_id].startswith("CUSTOM_") for f in fs)
+        assert n_custom > 200
+    finally:
+        eng.close()
 
 
 @pytest.mark.gpu

@@ -1,8 +1,11 @@
 """Window re-scan (a12) on the GPU vs the oracle's full re-scan of the joined window.
 
-pii_rescan_window keeps each conversation's last N utterances (text + resident candidates) in HBM
-and scans only the new rows; the bar is bit-exact redacted window bytes, window spans and window
-context against oracle.process_window_rows, which re-redacts "\\n".join(window) from scratch.
+pii_rescan_window keeps each conversation's last N utterances in HBM.  Incremental mode (the shipped
+rules) keeps text + resident candidates and scans only the new rows; full mode (forced here with
+PII_WINDOW_FULL, and taken by any rule set the incremental path cannot handle: config 5's SCAN
+groups, a detector that consumes '\\n') materialises every "\\n"-joined window and runs it through
+the pipeline.  Both are checked against oracle.process_window_rows, which re-redacts
+"\\n".join(window) from scratch: bit-exact redacted window bytes, window spans and window context.
 """
 import random
 
@@ -13,11 +16,12 @@ from conftest import pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def weng(compiled):
+@pytest.fixture(scope="module", params=["incremental", "full"])
+def weng(compiled, request):
     E = pkg("engine")
     e = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
-    e.window_enable(5, 8192)
+    e.window_enable(5, 8192, full=request.param == "full")
+    assert e.window_mode() == request.param
     yield e
     e.close()
 
@@ -102,13 +106,14 @@ def test_window_halo_and_edges(weng, oracle_cfg):
     _check(weng, oracle_cfg, [[(901, C, b"SSN 123-45-6788", 9), (901, C, b"ok", 10)]], state=state)
 
 
-def test_window_history_overflow_is_atomic(compiled, oracle_cfg):
+@pytest.mark.parametrize("full", [False, True])
+def test_window_history_overflow_is_atomic(compiled, oracle_cfg, full):
     """a window that does not fit its slot fails the call and commits nothing"""
     from oracle import pii_oracle as O
     E = pkg("engine")
     eng = E.Engine(compiled.blob, device=0, n_conv_slots=8)
     try:
-        eng.window_enable(5, 256)
+        eng.window_enable(5, 256, full=full)
         C = O.ROLE_CUSTOMER
         eng.rescan_window([b"a" * 100], [1], [C], [1])
         assert eng.window_count(1) == 1
@@ -118,5 +123,61 @@ def test_window_history_overflow_is_atomic(compiled, oracle_cfg):
         assert eng.window_count(1) == 1
         res = eng.rescan_window([b"c" * 10], [1], [C], [3])
         assert res.text(0) == b"a" * 100 + b"\n" + b"c" * 10
+    finally:
+        eng.close()
+
+
+def test_window_with_a_newline_consuming_detector(oracle_cfg):
+    """a custom regex whose \\s can consume the '\\n' join (so a match can cross utterances of the
+    window): the engine takes the full path on its own and matches the oracle"""
+    import copy
+    import json
+    import os
+    import yaml
+    from oracle import pii_oracle as O
+    C = pkg("compiler")
+    E = pkg("engine")
+    rules_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "context-based-pii_amd",
+                             "rules")
+    cfg = json.load(open(os.path.join(rules_dir, "dlp_config.json")))
+    builtin = yaml.safe_load(open(os.path.join(rules_dir, "builtin_infotypes.yaml")))
+    cfg = copy.deepcopy(cfg)
+    cfg["inspect_config"]["custom_info_types"].append(
+        {"info_type": {"name": "ORDER_REFERENCE"}, "regex": {"pattern": "\\border\\s+ref\\s*:?\\s*\\d{6}\\b"},
+         "likelihood": "VERY_LIKELY"})
+    comp = C.compile_rules(C.Rules(cfg, builtin))
+    ocfg = O.RuleConfig(cfg, builtin)
+    eng = E.Engine(comp.blob, device=0, n_conv_slots=256)
+    try:
+        eng.window_enable(5, 8192)
+        assert eng.window_mode() == "full"
+        A, Cu = O.ROLE_AGENT, O.ROLE_CUSTOMER
+        r = random.Random(3)
+        synth = pkg("synth")
+        bank = synth.build_bank(200, 200, seed=3)
+        rows = []
+        for conv in range(40):
+            for k in range(9):
+                t = r.choice(bank.texts)
+                if r.random() < 0.3:
+                    t = t + b" my order ref"                  # the number follows in the next utterance
+                elif r.random() < 0.3:
+                    t = b"123456 " + t
+                elif r.random() < 0.2:
+                    t = b"order ref: 654321 " + t
+                rows.append((10 + conv, A if k % 2 == 0 else Cu, t, 1_000_000 * k))
+        by_conv = {}
+        for row in rows:
+            by_conv.setdefault(row[0], []).append(row)
+        state = None
+        crossed = 0
+        for k in range(9):
+            batch = [by_conv[c][k] for c in sorted(by_conv)]
+            state = _check(eng, ocfg, [batch], state=state)
+            for c in by_conv:                                    # the windows just re-scanned
+                win = b"\n".join(state[1][c])
+                crossed += any(ocfg.type_names[f.type_id] == "ORDER_REFERENCE" and b"\n" in win[f.start:f.end]
+                               for f in O.find_pii(win, ocfg))
+        assert crossed > 0                                       # some match did cross a join
     finally:
         eng.close()
