@@ -114,19 +114,67 @@ def source_digest() -> str:
     return h.hexdigest()[:16]
 
 
-def measured_traffic(kernel: str, n_bytes: int):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (tools/pmc_traffic.py), but only
-    when they were measured on exactly these kernel sources and this workload size; else None."""
+N_CU = 256                 # MI355X compute units
+CLOCK_HZ = 2.4e9           # engine clock under load (MI355X_MICROARCH.md)
+
+
+def _pmc_entry(workload: str, n_bytes: int):
+    """the committed PMC passes of `workload` (tools/pmc_traffic.py -> profiles/traffic.json), only when
+    measured on exactly these kernel sources and this workload size; else None"""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None
-    ks = t.get("kernels", {})
-    k = ks.get(kernel) or ks.get(kernel + "<true>")       # (k_scan is a template: k_scan<true> = SCAN group 0)
-    if not k or t.get("source_digest") != source_digest() or t.get("bytes_per_gpu") != n_bytes:
+    e = t.get("workloads", {}).get(workload)
+    if not e or e.get("source_digest") != source_digest() or e.get("bytes_per_gpu") != n_bytes:
         return None
-    return k.get("hbm_bytes")
+    return e
+
+
+def measured_traffic(kernel: str, n_bytes: int, workload: str = "scan"):
+    """HBM bytes per launch of `kernel` (a name prefix: k_scan covers every SCAN-group instantiation,
+    summed) from the workload's own PMC passes, or None"""
+    e = _pmc_entry(workload, n_bytes)
+    if e is None:
+        return None
+    ks = [v for k, v in e.get("kernels", {}).items() if k == kernel or k.startswith(kernel + "<")]
+    if not ks or any(v.get("hbm_bytes") is None for v in ks):
+        return None
+    return int(sum(v["hbm_bytes"] for v in ks))
+
+
+def measured_pipeline_traffic(n_bytes: int, workload: str = "scan"):
+    """HBM bytes of all engine kernels of one call (sum of their per-dispatch means), or None"""
+    e = _pmc_entry(workload, n_bytes)
+    if e is None:
+        return None
+    ks = [v.get("hbm_bytes") for v in e.get("kernels", {}).values() if v.get("hbm_bytes") is not None]
+    return int(sum(ks)) if ks else None
+
+
+def roofline_compute(n_bytes: int, scan_ms: float, workload: str = "scan"):
+    """k_scan's compute ceiling: the DFA step is bound by LDS-array cycles (three table reads per byte,
+    bank conflicts), not by HBM.  LDS-array cycles per launch come from the workload's PMC pass
+    (SQ_LDS_IDX_ACTIVE, converted with the tools/micro/lds_calib factor); all N_CU LDS arrays busy
+    every CLOCK_HZ cycle is the ceiling."""
+    e = _pmc_entry(workload, n_bytes)
+    if e is None or not e.get("lds_counter_per_cycle"):
+        return None
+    ks = [v for k, v in e["kernels"].items() if k.startswith("k_scan<") and v.get("lds_array_cycles")]
+    if not ks:
+        return None
+    cyc = sum(v["lds_array_cycles"] for v in ks)
+    conf = sum(v.get("lds_bank_conflict", 0) for v in ks) / max(1, sum(v.get("lds_idx_active", 0) for v in ks))
+    t_min = cyc / (N_CU * CLOCK_HZ)
+    ceiling = n_bytes / t_min / 1e9
+    achieved = n_bytes / (scan_ms / 1e3) / 1e9
+    return {"bound": "lds", "kernel": "k_scan", "achieved": round(achieved, 1), "peak": round(ceiling, 1),
+            "unit": "GB/s of input", "frac": round(achieved / ceiling, 4),
+            "lds_cycles_per_byte": round(cyc / n_bytes, 4), "bank_conflict_share": round(conf, 4),
+            "lds_cycles_per_launch": int(cyc),
+            "note": f"ceiling = input bytes / (LDS-array cycles / ({N_CU} CUs x {CLOCK_HZ / 1e9:g} GHz)); "
+                    "cycles from SQ_LDS_IDX_ACTIVE / tools/micro/lds_calib factor"}
 
 
 # --------------------------------------------------------------------------- GPU corpus assembly
@@ -280,7 +328,10 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
     # k_redact: input + output bytes, its offset/count reads, the span copy (read + write)
     red_B = n_bytes + ob + 8 * (n + 1) * 3 + 4 * n + 32 * ns
     red_GBps = red_B / max(k_ms["k_redact"] / 1e3, 1e-12) / 1e9
-    traffic = measured_traffic("k_scan", n_bytes)
+    wl = getattr(args, "workload", "scan")
+    traffic = measured_traffic("k_scan", n_bytes, wl)
+    pipe_traffic = measured_pipeline_traffic(n_bytes, wl)
+    rc = roofline_compute(n_bytes, k_ms["k_scan"], wl)
     return {
         "metric": METRIC, "value": round(mbps, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -301,12 +352,15 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
             ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
         "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
         "pipeline": {"algorithmic_bytes": int(Bw), "GBps": round(Bw / t_pipe / 1e9, 1),
-                     "frac": round(Bw / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "frac": round(Bw / t_pipe / 1e9 / HBM_PEAK_GBPS, 4), "traffic": pipe_traffic},
         "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(scan_GBps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes": int(scan_B), "launch_ms": round(k_ms["k_scan"], 4)},
+                     "algorithmic_bytes": int(scan_B), "launch_ms": round(k_ms["k_scan"], 4),
+                     "input_frac": round(n_bytes / (k_ms["k_scan"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "roofline_compute": rc,
         "roofline_redact": {"bound": "hbm", "kernel": "k_redact", "achieved": round(red_GBps, 1),
                             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(red_GBps / HBM_PEAK_GBPS, 4),
+                            "traffic": measured_traffic("k_redact", n_bytes, wl),
                             "algorithmic_bytes": int(red_B), "launch_ms": round(k_ms["k_redact"], 4)},
         "histogram": {"collective": "all_reduce u64[T+1] (RCCL)" if world > 1 else "none (1 rank)",
                       "total_spans_last_step": int(reduced[T]), "verified": verified,
@@ -342,7 +396,8 @@ def main():
     ap.add_argument("--cpu-gb", type=float, default=1.0, help="bytes the CPU baseline times (>= 1 GB, BASELINE.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="(config 3 baseline) CPU seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5", "ner", "ner-redact"],
+    ap.add_argument("--workload", choices=["scan", "window", "stream", "long", "config5", "ner", "ner-redact",
+                                           "service"],
                     default="scan",
                     help="scan = config 2 (headline); window = config 3 multi-turn re-scan; "
                          "stream = config 4 PCIe-inclusive batch stream; long = config-2 bytes as long rows; "
@@ -352,7 +407,10 @@ def main():
     ap.add_argument("--ner-batch", type=int, default=64, help="(ner) sequences per step")
     ap.add_argument("--ner-seq", type=int, default=128, help="(ner) tokens per sequence")
     ap.add_argument("--ner-rows", type=int, default=8192, help="(ner-redact) utterances per step")
+    ap.add_argument("--clients", type=int, default=64, help="(service) concurrent HTTP clients")
+    ap.add_argument("--requests", type=int, default=200, help="(service) requests per client")
     ap.add_argument("--window-n", type=int, default=5)
+    ap.add_argument("--window-full", action="store_true", help="(window) force the full re-scan of the joined windows")
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
     ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
     ap.add_argument("--shard-gb", type=float, default=1.0, help="(config 4) host shard each rank replays, GB")
@@ -367,6 +425,8 @@ def main():
         return ner_main(args)
     if args.workload == "ner-redact":
         return ner_redact_main(args)
+    if args.workload == "service":
+        return service_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
 
@@ -601,6 +661,110 @@ def ner_redact_main(args):
         "cpu_baseline": cpu,
     }
     eng.close()
+    print(json.dumps(line), flush=True)
+
+
+# --------------------------------------------------------------------------- the drop-in service
+def service_main(args):
+    """The Flask drop-in (app.py) on the engine, over real HTTP on 127.0.0.1: --clients threads, each a
+    keep-alive connection replaying its own conversation (agent question / customer answer
+    alternating, /handle-agent-utterance and /handle-customer-utterance), --requests each.  Reports
+    requests/s and latency percentiles, and the micro-batch sizes the batcher formed.  The
+    reference's deployment serves these routes with 1 gunicorn worker x 8 threads, one blocking DLP
+    RPC per request (main_service/Dockerfile:29): at most 8 requests in flight; its DLP latency is
+    not published, so no reference rate is quoted."""
+    import http.client
+    import threading
+    from werkzeug.serving import make_server
+    import torch
+    A = importlib.import_module("context-based-pii_amd.app")
+    S = importlib.import_module("context-based-pii_amd.service")
+    torch.cuda.set_device(0)
+    bank = synth.build_bank(4096, 4096, seed=synth.SEED)
+    svc = S.PiiService(n_slots=1 << 14)
+    app = A.create_app(svc, max_batch=1024, max_wait_s=0.0005)
+    srv = make_server("127.0.0.1", 0, app, threaded=True)
+    port = srv.server_port
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    C, R = args.clients, args.requests
+    lat = [[] for _ in range(C)]
+    nbytes = [0] * C
+    errors = [0] * C
+
+    def client(k, n, record):
+        import random
+        r = random.Random(k)
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        for j in range(n):
+            agent = j % 2 == 0
+            text = r.choice(bank.texts[:4096] if agent else bank.texts[4096:]).decode()
+            body = json.dumps({"conversation_id": f"c{k}", "transcript": text})
+            t0 = time.perf_counter()
+            conn.request("POST", "/handle-agent-utterance" if agent else "/handle-customer-utterance", body,
+                         {"Content-Type": "application/json"})
+            resp = conn.getresponse()
+            resp.read()
+            if record:
+                lat[k].append(time.perf_counter() - t0)
+                nbytes[k] += len(text.encode())
+                errors[k] += resp.status != 200
+        conn.close()
+
+    def run(n, record):
+        ts = [threading.Thread(target=client, args=(k, n, record)) for k in range(C)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return time.perf_counter() - t0
+    run(max(2, R // 10), False)                    # warmup: engine buffers, connections
+    batcher = app.config["PII_BATCHER"]
+    batcher.batches.clear()
+    el = run(R, True)
+    srv.shutdown()
+    all_lat = np.sort(np.concatenate([np.array(x) for x in lat])) * 1e3
+    n_req = len(all_lat)
+    sizes = np.array(batcher.batches)
+    # the same requests through PiiService.process_requests directly (no HTTP, no batcher): the ceiling
+    # the Python front end leaves
+    import random
+    r = random.Random(0)
+    reqs = []
+    for j in range(R):
+        for k in range(C):
+            agent = j % 2 == 0
+            reqs.append(("agent" if agent else "customer",
+                         {"conversation_id": f"d{k}", "transcript": r.choice(bank.texts[:4096] if agent else
+                                                                           bank.texts[4096:]).decode()}))
+    svc.process_requests(reqs[:C * 2])
+    t0 = time.perf_counter()
+    for i in range(0, len(reqs), 1024):
+        svc.process_requests(reqs[i:i + 1024])
+    direct = len(reqs) / (time.perf_counter() - t0)
+    batcher.close()
+    line = {
+        "metric": "drop-in service: requests/s through the Flask shim (app.py) on one MI355X, with latency",
+        "value": round(n_req / el, 1), "unit": "requests/s", "n_gpus": 1, "steps": R, "warmup": max(2, R // 10),
+        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"{C} HTTP/1.1 keep-alive clients on 127.0.0.1 x {R} requests, each client one "
+                               f"conversation alternating /handle-agent-utterance and /handle-customer-utterance "
+                               f"(config-2 utterances), werkzeug threaded server, MicroBatcher(max_batch=1024, "
+                               f"max_wait=0.5 ms)", "clients": C},
+        "latency_ms": {"p50": round(float(np.percentile(all_lat, 50)), 3),
+                       "p90": round(float(np.percentile(all_lat, 90)), 3),
+                       "p99": round(float(np.percentile(all_lat, 99)), 3), "max": round(float(all_lat[-1]), 3)},
+        "transcript_MBps": round(sum(nbytes) / el / 1e6, 3),
+        "errors": int(sum(errors)),
+        "micro_batches": {"count": int(len(sizes)), "mean_size": round(float(sizes.mean()), 2) if len(sizes) else 0,
+                          "max_size": int(sizes.max()) if len(sizes) else 0},
+        "process_requests_direct_per_s": round(direct, 1),
+        "reference_concurrency": "1 gunicorn worker x 8 threads = at most 8 DLP RPCs in flight "
+                                 "(main_service/Dockerfile:29); the DLP latency is not published",
+    }
+    svc.engine.close()
     print(json.dumps(line), flush=True)
 
 
@@ -887,7 +1051,7 @@ def window_main(args):
     d_ctx = torch.empty(C, dtype=torch.int16, device=dev)
     comp = compiler.compile_default()
     eng = eng_mod.Engine(comp.blob, device=0, n_conv_slots=C)
-    eng.window_enable(N, 8192)
+    eng.window_enable(N, 8192, full=args.window_full)
     torch.cuda.synchronize()
 
     def step(k):
@@ -941,8 +1105,10 @@ def window_main(args):
         "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"config3: {C} concurrent conversations, window N={N}, one new utterance per "
-                               f"conversation per step (pii_rescan_window_device), expected_pii_type context",
-                   "rows_per_step": C, "parallelism": "conversation-sharded x1"},
+                               f"conversation per step (pii_rescan_window_device, {eng.window_mode()} mode), "
+                               f"expected_pii_type context",
+                   "rows_per_step": C, "parallelism": "conversation-sharded x1",
+                   "bytes_per_gpu": int(meta.offsets[-1])},
         "windows_per_s": round(K * C / elapsed, 1),
         "window_output_MBps": round(out_b / elapsed / 1e6, 1),
         "naive_equivalent_bytes_rescanned_per_step": int(win_in / K),
@@ -950,10 +1116,12 @@ def window_main(args):
         "stages_ms": {k: round(float(v), 4) for k, v in zip(
             ["scan+pairs", "context", "first+cands", "select+offsets", "redact+commit", "pipeline"], per_stage)},
         "pipeline": {"algorithmic_bytes": int(B / K), "GBps": round(B / t_pipe / 1e9, 1),
-                     "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4),
+                     "traffic": measured_pipeline_traffic(int(meta.offsets[-1]), "window")},
         "roofline": {"bound": "hbm", "kernel": "k_win_redact", "achieved": round(red_B / K / (k_red / 1e3) / 1e9, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(red_B / K / (k_red / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "frac": round(red_B / K / (k_red / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "traffic": measured_traffic("k_win_redact", int(meta.offsets[-1]), "window"),
                      "algorithmic_bytes": int(red_B / K), "launch_ms": round(k_red, 4)},
         "cpu_baseline": cpu,
     }

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/pii_engine.h"
@@ -3911,6 +3912,9 @@ struct pii_engine {
     uint32_t cap_j_utt = 0;
     uint32_t* err_saved = nullptr;
     uint64_t* h_jtotal = nullptr;      // pinned: the joined bytes of the call
+    // work-buffer accounting (grow): bytes per buffer, their sum, the limit (0 = none)
+    std::unordered_map<void*, size_t> scratch_sizes;
+    uint64_t scratch_used = 0, scratch_limit = 0;
     // lane-based resolve, long rows, span-driven redaction
     uint32_t r0 = 0, long_min = NO_CUTS;
     uint32_t* long_rows = nullptr;     // rows cut into several lanes (k_chunk_index)
@@ -3942,15 +3946,36 @@ struct pii_engine {
 
 namespace {
 
+// (Re)size a work buffer.  The new buffer is allocated before the old one is freed, so a failure
+// leaves the old buffer -- and the capacity the caller recorded for it -- intact; the engine stays
+// usable for calls that fit.  Work buffers count against the scratch limit (pii_set_scratch_limit).
 template <class T>
 int grow(pii_engine* e, T*& p, size_t count) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
     if (count == 0) count = 1;
-    if (hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)) != hipSuccess) {
+    const size_t nb = count * sizeof(T);
+    size_t old = 0;
+    if (p) {
+        auto it = e->scratch_sizes.find(static_cast<void*>(p));
+        if (it != e->scratch_sizes.end()) old = it->second;
+    }
+    if (e->scratch_limit && e->scratch_used - old + nb > e->scratch_limit) {
+        e->err = "device allocation failed: the engine's work buffers would exceed its scratch limit";
+        return PII_E_NOMEM;
+    }
+    T* q = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&q), nb) != hipSuccess) {
+        (void)hipGetLastError();
         e->err = "device allocation failed";
         return PII_E_NOMEM;
     }
+    if (p) {
+        (void)hipFree(p);
+        e->scratch_sizes.erase(static_cast<void*>(p));
+        e->scratch_used -= old;
+    }
+    p = q;
+    e->scratch_sizes[static_cast<void*>(q)] = nb;
+    e->scratch_used += nb;
     return PII_OK;
 }
 
@@ -5328,6 +5353,18 @@ int pii_window_enable_ex(pii_engine* e, uint32_t window_n, uint32_t slot_bytes, 
 
 int pii_window_enable(pii_engine* e, uint32_t window_n, uint32_t slot_bytes) {
     return pii_window_enable_ex(e, window_n, slot_bytes, 0);
+}
+
+int pii_set_scratch_limit(pii_engine* e, uint64_t bytes) {
+    if (!e) return PII_E_ARG;
+    e->scratch_limit = bytes;
+    return PII_OK;
+}
+
+int pii_scratch_bytes(pii_engine* e, uint64_t* used) {
+    if (!e || !used) return PII_E_ARG;
+    *used = e->scratch_used;
+    return PII_OK;
 }
 
 int pii_window_mode(pii_engine* e) {

@@ -27,7 +27,7 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
            "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext", "pii_window_enable_ex",
-           "pii_window_mode"]
+           "pii_window_mode", "pii_set_scratch_limit", "pii_scratch_bytes"]
 PII_WINDOW_FULL = 1
 
 
@@ -100,6 +100,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_window_enable.argtypes = [P, c.c_uint32, c.c_uint32]
     lib.pii_window_enable_ex.argtypes = [P, c.c_uint32, c.c_uint32, c.c_uint32]
     lib.pii_window_mode.argtypes = [P]
+    lib.pii_set_scratch_limit.argtypes = [P, c.c_uint64]
+    lib.pii_scratch_bytes.argtypes = [P, U64]
     lib.pii_window_reset.argtypes = [P, c.c_uint32]
     lib.pii_window_count.argtypes = [P, c.c_uint32, U32]
     lib.pii_rescan_window.argtypes = lib.pii_scan_redact.argtypes
@@ -321,6 +323,19 @@ class Engine:
         rc = self.lib.pii_reserve(self.h, max_utt, max_bytes, max_out, max_spans)
         if rc != PII_OK:
             raise self._err(rc, "pii_reserve")
+
+    def set_scratch_limit(self, n_bytes: int) -> None:
+        """bound the work buffers' device memory (0 = none): calls that need more fail with PII_E_NOMEM"""
+        rc = self.lib.pii_set_scratch_limit(self.h, int(n_bytes))
+        if rc != PII_OK:
+            raise self._err(rc, "pii_set_scratch_limit")
+
+    def scratch_bytes(self) -> int:
+        v = ctypes.c_uint64()
+        rc = self.lib.pii_scratch_bytes(self.h, ctypes.byref(v))
+        if rc != PII_OK:
+            raise self._err(rc, "pii_scratch_bytes")
+        return int(v.value)
 
     def sync(self) -> Tuple[int, int, int]:
         tot = (ctypes.c_uint64 * 3)()

@@ -350,12 +350,19 @@ class PiiService:
                 res = self._run([_enc(r[2]) for r in rows], [r[0] for r in rows], [r[3] for r in rows],
                                 [now] * len(rows))
             except PiiError as e:
+                # The reference's handlers never fail on a DLP error: the error string is the transcript
+                # (main.py:752-773) and context_used reports the Redis GET (main.py:425).  The engine
+                # call is atomic, so a failed call stores no context (context_stored False).
                 for slot, i, text, role, split_last in rows:
                     kind, data = reqs[i]
                     if kind == "agent":
                         out[i] = ({"redacted_transcript": error_string(e.code, text), "context_stored": False}, 200)
                     elif kind == "customer":
-                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_used": False}, 200)
+                        try:
+                            used = self._context_record(slot, now) is not None
+                        except PiiError:
+                            used = False
+                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_used": used}, 200)
                     else:                                   # main.py:458-461 on the error string
                         red = error_string(e.code, text)
                         lines = red.splitlines() if split_last else [red]

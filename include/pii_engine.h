@@ -146,6 +146,13 @@ int pii_scan_redact_device_ext(struct pii_engine* e, const uint8_t* d_bytes, con
  * hipMalloc, which synchronizes the device, inside a streaming loop).  The pair / event queues still
  * grow on overflow (pii_sync re-runs the batch) -- their need depends on the text, not its size. */
 int pii_reserve(struct pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint64_t max_out, uint32_t max_spans);
+/* Bound the device memory of the engine's per-call work buffers (queues, arenas, staging; not the rules
+ * or the context / window tables), e.g. on a GPU shared with other work; 0 = no limit.  A call that
+ * would need more fails with PII_E_NOMEM and commits nothing (the service maps it to
+ * "[DLP_PROCESSING_ERROR] {transcript}", main.py:770-773); buffers already held stay valid.
+ * pii_scratch_bytes reports what the work buffers hold now. */
+int pii_set_scratch_limit(struct pii_engine* e, uint64_t bytes);
+int pii_scratch_bytes(struct pii_engine* e, uint64_t* used);
 /* wait for the last device call; totals[0] = output bytes, [1] = spans, [2] = error flags */
 int pii_sync(struct pii_engine* e, uint64_t totals[3]);
 

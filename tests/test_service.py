@@ -521,3 +521,53 @@ def test_flask_concurrent_requests_on_gpu(oracle_cfg):
         assert [b["redacted_transcript"] for b in got[cid]] == want, cid
     assert max(app.config["PII_BATCHER"].batches) > 1
     app.config["PII_BATCHER"].close()
+
+
+@pytest.mark.gpu
+def test_service_maps_engine_nomem_and_capacity_to_processing_error(oracle_cfg):
+    """The engine runs out of device memory (its work buffers capped with pii_set_scratch_limit) inside
+    a batch, a handler call and a queue-overflow re-run: every row gets the reference's
+    "[DLP_PROCESSING_ERROR] {transcript}" (main.py:770-773), nothing is committed, and the same calls
+    succeed once the limit is lifted.  A device call whose output buffer is too small reports
+    PII_E_CAPACITY, which maps to the same string."""
+    import torch
+    from oracle import pii_oracle as O
+    S, E = pkg("service"), pkg("engine")
+    svc = S.PiiService(n_slots=64, clock=Clock(), time_base="payload")
+    eng = svc.engine
+    small = [{"conversation_id": "s", "participant_role": "AGENT", "text": "What is your email address?",
+              "start_timestamp_usec": 1}]
+    assert svc.process_batch(small) == ["What is your email address?"]
+    eng.set_scratch_limit(eng.scratch_bytes())                 # no room to grow any work buffer
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    texts = [e["text"] for t in tr.values() for e in t["entries"]] * 400             # ~0.5 MB
+    big = [{"conversation_id": f"b{i // 20}", "participant_role": "AGENT" if i % 2 == 0 else "END_USER",
+            "text": t, "start_timestamp_usec": 10 + i} for i, t in enumerate(texts)]
+    out = svc.process_batch(big)
+    assert out == [f"[DLP_PROCESSING_ERROR] {r['text']}" for r in big]
+    long_t = " ".join(texts[:2000])
+    body, code = svc.handle_customer_utterance({"conversation_id": "s", "transcript": long_t})
+    # (context_used reports the context record, as the reference's Redis GET does, main.py:425)
+    assert code == 200 and body == {"redacted_transcript": f"[DLP_PROCESSING_ERROR] {long_t}", "context_used": True}
+    assert eng.context_get(svc.slots.peek("b0"))[0] == -1      # the failed batch stored no context
+    eng.set_scratch_limit(0)
+    out = svc.process_batch(big)
+    rows = [(r["conversation_id"], O.ROLE_AGENT if r["participant_role"] == "AGENT" else O.ROLE_CUSTOMER,
+             r["text"].encode(), r["start_timestamp_usec"]) for r in big]
+    assert out == [x[0].decode() for x in O.process_rows(rows, oracle_cfg)]
+    # PII_E_CAPACITY from the device entry point (a caller-sized output buffer that is too small)
+    data, offs = E.pack([b"my email is jane.doe@example.com"] * 4)
+    dev = torch.device("cuda:0")
+    d_t = torch.from_numpy(np.concatenate([data, np.zeros(64, np.uint8)])).to(dev)
+    d_o = torch.from_numpy(offs.view(np.int64)).to(dev)
+    z32, z8, z64 = (torch.zeros(4, dtype=d, device=dev) for d in (torch.int32, torch.uint8, torch.int64))
+    out_b = torch.empty(16, dtype=torch.uint8, device=dev)
+    oo = torch.empty(5, dtype=torch.int64, device=dev)
+    sp = torch.empty(64 * 16, dtype=torch.uint8, device=dev)
+    eng.scan_redact_device_ex(d_t.data_ptr(), d_o.data_ptr(), 4, 0, int(offs[-1]), z32.data_ptr(), z8.data_ptr(),
+                              z64.data_ptr(), out_b.data_ptr(), 16, oo.data_ptr(), sp.data_ptr(), 64)
+    with pytest.raises(E.PiiError) as ei:
+        eng.sync()
+    assert ei.value.code == E.PII_E_CAPACITY
+    assert S.error_string(ei.value.code, "x") == "[DLP_PROCESSING_ERROR] x"
+    eng.close()
