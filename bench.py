@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 synth = importlib.import_module("context-based-pii_amd.synth")
 compiler = importlib.import_module("context-based-pii_amd.compiler")
+distributed = importlib.import_module("context-based-pii_amd.distributed")
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy ceiling
 LANE_BYTES = 1024        # BYTES_PER_LANE of csrc/pii_engine.hip (k_scan lane = utterances starting in 1 KiB)
@@ -207,13 +208,19 @@ def _sync(dev):
 
 
 class DeviceBatch:
-    """One rank's resident config-2 shard: conversations [conv_base, conv_base + C) of the synthetic
-    corpus (gpu = conversation_id % G on a dense id space is a contiguous block here),
-    staged into device memory once, plus the output buffers."""
+    """One rank's resident config-2 shard, staged into device memory once, plus the output buffers.
+    The node's conversations have dense global ids and are sharded as everywhere else
+    (distributed.shard_of, SURVEY §8(e): rank = id % world): rank r owns ids r, r + world, ...,
+    r + (C - 1) world, kept in its context slots 0..C-1 (slot k = id // world).  Their text is the
+    synthetic corpus generated for that rank (seed offset rank * C), so ranks hold different data."""
 
-    def __init__(self, C, U, bank, conv_base, dev, join: int = 1):
+    def __init__(self, C, U, bank, conv_base, dev, join: int = 1, rank: int = 0, world: int = 1):
         import torch
         self.meta = synth.corpus_meta(C, U, bank, seed=synth.SEED, conv_base=conv_base)
+        local = (self.meta.conv_slot - conv_base).astype(np.int64)
+        self.conversation_ids = rank + world * np.arange(C, dtype=np.int64)     # global ids this rank owns
+        assert all(distributed.shard_of(int(i), world) == rank for i in self.conversation_ids[:64])
+        assert (self.conversation_ids[local] // world == local).all()
         self.text, self.offs = gpu_corpus(self.meta, bank, dev)
         self.n = self.meta.n
         self.n_bytes = int(self.meta.offsets[-1])
@@ -257,7 +264,7 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
         bank = synth.build_bank(args.bank, args.bank, seed=synth.SEED)
     C, U = args.conversations, args.utt_per_conv
     join = max(1, int(getattr(args, "row_kb", 0) * 1024 / CFG2_MEAN_LEN)) if getattr(args, "workload", "") == "long" else 1
-    B = DeviceBatch(C, U, bank, rank * C, dev, join=join)
+    B = DeviceBatch(C, U, bank, rank * C, dev, join=join, rank=rank, world=world)
     eng = make_engine(B, bank, C)
     T = len(eng.type_names)
     hist = torch.zeros(T + 1, dtype=torch.int64, device=dev)
@@ -409,6 +416,7 @@ def main():
     ap.add_argument("--ner-rows", type=int, default=8192, help="(ner-redact) utterances per step")
     ap.add_argument("--clients", type=int, default=64, help="(service) concurrent HTTP clients")
     ap.add_argument("--requests", type=int, default=200, help="(service) requests per client")
+    ap.add_argument("--batch-wait-ms", type=float, default=0.5, help="(service) MicroBatcher max_wait")
     ap.add_argument("--window-n", type=int, default=5)
     ap.add_argument("--window-full", action="store_true", help="(window) force the full re-scan of the joined windows")
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
@@ -609,7 +617,11 @@ def ner_redact_main(args):
     d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
     d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
     d_ctx = torch.empty(n, dtype=torch.int16, device=dev)
-    st = torch.cuda.current_stream(dev)
+    # one explicit stream for the detector and the engine: a NULL stream handle would select the
+    # engine's own stream, which is not ordered after the detector's kernels
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(st)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     acc = np.zeros(2)
 
@@ -682,7 +694,9 @@ def service_main(args):
     torch.cuda.set_device(0)
     bank = synth.build_bank(4096, 4096, seed=synth.SEED)
     svc = S.PiiService(n_slots=1 << 14)
-    app = A.create_app(svc, max_batch=1024, max_wait_s=0.0005)
+    app = A.create_app(svc, max_batch=1024, max_wait_s=args.batch_wait_ms / 1e3)
+    import logging
+    logging.getLogger("werkzeug").setLevel(logging.ERROR)
     srv = make_server("127.0.0.1", 0, app, threaded=True)
     port = srv.server_port
     th = threading.Thread(target=srv.serve_forever, daemon=True)
@@ -752,7 +766,8 @@ def service_main(args):
         "config": {"workload": f"{C} HTTP/1.1 keep-alive clients on 127.0.0.1 x {R} requests, each client one "
                                f"conversation alternating /handle-agent-utterance and /handle-customer-utterance "
                                f"(config-2 utterances), werkzeug threaded server, MicroBatcher(max_batch=1024, "
-                               f"max_wait=0.5 ms)", "clients": C},
+                               f"max_wait={args.batch_wait_ms:g} ms)", "clients": C,
+                   "batch_wait_ms": args.batch_wait_ms},
         "latency_ms": {"p50": round(float(np.percentile(all_lat, 50)), 3),
                        "p90": round(float(np.percentile(all_lat, 90)), 3),
                        "p99": round(float(np.percentile(all_lat, 99)), 3), "max": round(float(all_lat[-1]), 3)},

@@ -3,7 +3,9 @@ against the oracle (the bench only checked error flags at thi
 
 The engine runs the batch once through the device API (exactly bench.DeviceBatch.run); the oracle
 replays all 100k conversations (oracle.process_rows, the reference's two handlers in order) on a
-fork pool of the host's CPU share.  Both sides reduce each conversation to one digest over its
+pool of the host's CPU share.  The pool's workers are SPAWNED (fresh interpreters that never touched
+HIP: this pytest process has initialised the GPU by the time these tests run) and read the corpus
+through memory-mapped .npy files.  Both sides reduce each conversation to one digest over its
 redacted bytes, its spans (16-byte pii_span records, utt = batch row) and its per-row context
 (ctx_info), so 10M rows are compared without holding the oracle's output."""
 import hashlib
@@ -18,6 +20,27 @@ from conftest import ROOT, pkg
 pytestmark = pytest.mark.gpu
 
 _W = {}
+
+
+def _init_worker(paths):
+    """spawned pool worker: the corpus arrays, memory-mapped (no copy per worker)"""
+    for k, path in paths.items():
+        _W[k] = np.load(path, mmap_mode="r") if path.endswith(".npy") else int(open(path).read())
+
+
+def _spawn_pool(arrays, cores):
+    """a pool of fresh interpreters over `arrays` (saved once as .npy files); returns (pool, tmpdir)"""
+    import tempfile
+    d = tempfile.mkdtemp(prefix="pii_fullsize_")
+    paths = {}
+    for k, v in arrays.items():
+        if isinstance(v, int):
+            paths[k] = os.path.join(d, k + ".int")
+            open(paths[k], "w").write(str(v))
+        else:
+            paths[k] = os.path.join(d, k + ".npy")
+            np.save(paths[k], np.ascontiguousarray(v))
+    return mp.get_context("spawn").Pool(cores, initializer=_init_worker, initargs=(paths,)), d
 
 
 def _digest(out: bytes, spans: bytes, ctx: bytes) -> bytes:
@@ -72,15 +95,19 @@ def test_config2_full_batch_every_row_vs_oracle():
     got = [_digest(out[int(oo[c * U]):int(oo[(c + 1) * U])].tobytes(),
                    sp[int(starts[c]):int(starts[c + 1])].tobytes(), ctx[c * U:(c + 1) * U].tobytes())
            for c in range(C)]
-    # oracle: all conversations, fork pool (no exec; workers only touch numpy and re)
-    _W.update(data=B.text[:B.n_bytes].cpu().numpy(), offs=B.meta.offsets.astype(np.int64), role=B.meta.role,
-              conv=B.meta.conv_slot, ts=B.meta.ts_us, U=U)
+    # oracle: all conversations on a pool of spawned workers (see the module docstring)
+    import shutil
     cores = bench.cpu_share()
     blocks = [(c, min(c + 250, C)) for c in range(0, C, 250)]
     want = [None] * C
-    with mp.get_context("fork").Pool(cores) as pool:
-        for c0, digs in pool.imap_unordered(_oracle_block, blocks):
-            want[c0:c0 + len(digs)] = digs
+    pool, tmp = _spawn_pool(dict(data=B.text[:B.n_bytes].cpu().numpy(), offs=B.meta.offsets.astype(np.int64),
+                                 role=B.meta.role, conv=B.meta.conv_slot, ts=B.meta.ts_us, U=U), cores)
+    try:
+        with pool:
+            for c0, digs in pool.imap_unordered(_oracle_block, blocks):
+                want[c0:c0 + len(digs)] = digs
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
     bad = [c for c in range(C) if got[c] != want[c]]
     assert not bad, (len(bad), bad[:10])
     assert ns > 1_000_000
@@ -136,11 +163,15 @@ def test_config3_window_rescan_100k_conversations_vs_oracle():
             hs[c].update(str(int(res.ctx_info[c])).encode())
     eng.close()
     got = [h.digest() for h in hs]
-    _W.update(wdata=data, woffs=o, wrole=meta.role, wts=meta.ts_us, wU=U, wN=N)
+    import shutil
     blocks = [(c, min(c + 500, C)) for c in range(0, C, 500)]
     want = [None] * C
-    with mp.get_context("fork").Pool(bench.cpu_share()) as pool:
-        for c0, digs in pool.imap_unordered(_oracle_window_block, blocks):
-            want[c0:c0 + len(digs)] = digs
+    pool, tmp = _spawn_pool(dict(wdata=data, woffs=o, wrole=meta.role, wts=meta.ts_us, wU=U, wN=N), bench.cpu_share())
+    try:
+        with pool:
+            for c0, digs in pool.imap_unordered(_oracle_window_block, blocks):
+                want[c0:c0 + len(digs)] = digs
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
     bad = [c for c in range(C) if got[c] != want[c]]
     assert not bad, (len(bad), bad[:10])

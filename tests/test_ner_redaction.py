@@ -256,7 +256,12 @@ def test_device_ner_on_the_redaction_path(eng, oracle_cfg, ner_model):
     S = 64
     data, offs, d_text, d_offs = _device_rows(texts)
     dev = m.dev
-    ext, ext_n, stride = m.detect_device(d_text.data_ptr(), d_offs.data_ptr(), n, S=S, info_type=P)
+    # one explicit stream for the detector and the engine (a NULL stream handle would select the
+    # engine's own stream, which is not ordered after the detector's kernels)
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(st):
+        ext, ext_n, stride = m.detect_device(d_text.data_ptr(), d_offs.data_ptr(), n, S=S, info_type=P)
     d_slot = torch.tensor([c + 100 for c, _, _, _ in rows], dtype=torch.int32, device=dev)
     d_role = torch.tensor([x for _, x, _, _ in rows], dtype=torch.uint8, device=dev)
     d_ts = torch.tensor([s for _, _, _, s in rows], dtype=torch.int64, device=dev)
@@ -269,8 +274,10 @@ def test_device_ner_on_the_redaction_path(eng, oracle_cfg, ner_model):
     eng.scan_redact_device_ext(d_text.data_ptr(), d_offs.data_ptr(), n, 0, int(offs[-1]), d_slot.data_ptr(),
                                d_role.data_ptr(), d_ts.data_ptr(), d_out.data_ptr(), out_cap, d_oo.data_ptr(),
                                d_sp.data_ptr(), span_cap, d_ctx.data_ptr(), ext.data_ptr(), ext_n.data_ptr(), stride,
-                               torch.cuda.current_stream(dev).cuda_stream)
+                               st.cuda_stream)
+    assert st.cuda_stream != 0
     ob, ns, fl = eng.sync()
+    st.synchronize()
     assert fl == 0
     out = d_out[:ob].cpu().numpy().tobytes()
     oo = d_oo.cpu().numpy()
