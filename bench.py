@@ -677,72 +677,102 @@ def ner_redact_main(args):
 
 
 # --------------------------------------------------------------------------- the drop-in service
-def service_main(args):
-    """The Flask drop-in (app.py) on the engine, over real HTTP on 127.0.0.1: --clients threads, each a
-    keep-alive connection replaying its own conversation (agent question / customer answer
-    alternating, /handle-agent-utterance and /handle-customer-utterance), --requests each.  Reports
-    requests/s and latency percentiles, and the micro-batch sizes the batcher formed.  The
-    reference's deployment serves these routes with 1 gunicorn worker x 8 threads, one blocking DLP
-    RPC per request (main_service/Dockerfile:29): at most 8 requests in flight; its DLP latency is
-    not published, so no reference rate is quoted."""
+def _service_client(port, k0, n_threads, n, texts_a, texts_c, out_q):
+    """one client PROCESS (spawned: it never touches the GPU): n_threads keep-alive connections, each
+    replaying its own conversation; reports (latencies, bytes, errors)"""
     import http.client
+    import random
     import threading
-    from werkzeug.serving import make_server
-    import torch
-    A = importlib.import_module("context-based-pii_amd.app")
-    S = importlib.import_module("context-based-pii_amd.service")
-    torch.cuda.set_device(0)
-    bank = synth.build_bank(4096, 4096, seed=synth.SEED)
-    svc = S.PiiService(n_slots=1 << 14)
-    app = A.create_app(svc, max_batch=1024, max_wait_s=args.batch_wait_ms / 1e3)
-    import logging
-    logging.getLogger("werkzeug").setLevel(logging.ERROR)
-    srv = make_server("127.0.0.1", 0, app, threaded=True)
-    port = srv.server_port
-    th = threading.Thread(target=srv.serve_forever, daemon=True)
-    th.start()
-    C, R = args.clients, args.requests
-    lat = [[] for _ in range(C)]
-    nbytes = [0] * C
-    errors = [0] * C
+    lat, nb, err = [], [0], [0]
+    lock = threading.Lock()
 
-    def client(k, n, record):
-        import random
+    def one(k):
         r = random.Random(k)
-        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=120)
+        mine = []
+        b = e = 0
         for j in range(n):
             agent = j % 2 == 0
-            text = r.choice(bank.texts[:4096] if agent else bank.texts[4096:]).decode()
+            text = r.choice(texts_a if agent else texts_c)
             body = json.dumps({"conversation_id": f"c{k}", "transcript": text})
             t0 = time.perf_counter()
             conn.request("POST", "/handle-agent-utterance" if agent else "/handle-customer-utterance", body,
                          {"Content-Type": "application/json"})
             resp = conn.getresponse()
             resp.read()
-            if record:
-                lat[k].append(time.perf_counter() - t0)
-                nbytes[k] += len(text.encode())
-                errors[k] += resp.status != 200
+            mine.append(time.perf_counter() - t0)
+            b += len(text.encode())
+            e += resp.status != 200
         conn.close()
+        with lock:
+            lat.extend(mine)
+            nb[0] += b
+            err[0] += e
+    ts = [threading.Thread(target=one, args=(k0 + i,)) for i in range(n_threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    out_q.put((lat, nb[0], err[0]))
 
-    def run(n, record):
-        ts = [threading.Thread(target=client, args=(k, n, record)) for k in range(C)]
-        t0 = time.perf_counter()
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        return time.perf_counter() - t0
-    run(max(2, R // 10), False)                    # warmup: engine buffers, connections
+
+def service_main(args):
+    """The Flask drop-in (app.py) on the engine, over real HTTP on 127.0.0.1: --clients connections
+    spread over spawned client processes (so the clients do not share the server's interpreter), each
+    replaying its own conversation (agent question / customer answer alternating,
+    /handle-agent-utterance and /handle-customer-utterance), --requests each.  Reports requests/s and
+    latency percentiles, and the micro-batch sizes the batcher formed.  The reference's deployment
+    serves these routes with 1 gunicorn worker x 8 threads, one blocking DLP RPC per request
+    (main_service/Dockerfile:29): at most 8 requests in flight; its DLP latency is not published, so
+    no reference rate is quoted."""
+    import threading
+    import logging
+    from werkzeug.serving import make_server
+    bank = synth.build_bank(4096, 4096, seed=synth.SEED)
+    texts_a = [t.decode() for t in bank.texts[:4096]]
+    texts_c = [t.decode() for t in bank.texts[4096:]]
+    C, R = args.clients, args.requests
+    n_proc = max(1, min(C, cpu_share() // 2))
+    ctx = mp.get_context("spawn")
+    import torch
+    A = importlib.import_module("context-based-pii_amd.app")
+    S = importlib.import_module("context-based-pii_amd.service")
+    torch.cuda.set_device(0)
+    svc = S.PiiService(n_slots=1 << 14)
+    app = A.create_app(svc, max_batch=1024, max_wait_s=args.batch_wait_ms / 1e3)
+    logging.getLogger("werkzeug").setLevel(logging.ERROR)
+    srv = make_server("127.0.0.1", 0, app, threaded=True)
+    port = srv.server_port
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
     batcher = app.config["PII_BATCHER"]
+
+    def run(n):
+        q = ctx.Queue()
+        per = [C // n_proc + (1 if i < C % n_proc else 0) for i in range(n_proc)]
+        ps, k0 = [], 0
+        for i in range(n_proc):
+            ps.append(ctx.Process(target=_service_client, args=(port, k0, per[i], n, texts_a, texts_c, q)))
+            k0 += per[i]
+        t0 = time.perf_counter()
+        for p in ps:
+            p.start()
+        res = [q.get() for _ in ps]
+        el = time.perf_counter() - t0
+        for p in ps:
+            p.join()
+        return el, res
+    run(max(2, R // 10))                           # warmup: engine buffers, connections, interpreters
     batcher.batches.clear()
-    el = run(R, True)
+    el, res = run(R)
     srv.shutdown()
-    all_lat = np.sort(np.concatenate([np.array(x) for x in lat])) * 1e3
+    all_lat = np.sort(np.concatenate([np.array(r[0]) for r in res])) * 1e3
     n_req = len(all_lat)
+    nbytes = sum(r[1] for r in res)
+    errors = sum(r[2] for r in res)
     sizes = np.array(batcher.batches)
-    # the same requests through PiiService.process_requests directly (no HTTP, no batcher): the ceiling
-    # the Python front end leaves
+    # the same kind of requests through PiiService.process_requests directly (no HTTP, no batcher),
+    # in micro-batches of 1024: the rate the engine path itself sustains
     import random
     r = random.Random(0)
     reqs = []
@@ -750,8 +780,7 @@ def service_main(args):
         for k in range(C):
             agent = j % 2 == 0
             reqs.append(("agent" if agent else "customer",
-                         {"conversation_id": f"d{k}", "transcript": r.choice(bank.texts[:4096] if agent else
-                                                                           bank.texts[4096:]).decode()}))
+                         {"conversation_id": f"d{k}", "transcript": r.choice(texts_a if agent else texts_c)}))
     svc.process_requests(reqs[:C * 2])
     t0 = time.perf_counter()
     for i in range(0, len(reqs), 1024):
@@ -763,16 +792,16 @@ def service_main(args):
         "value": round(n_req / el, 1), "unit": "requests/s", "n_gpus": 1, "steps": R, "warmup": max(2, R // 10),
         "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": f"{C} HTTP/1.1 keep-alive clients on 127.0.0.1 x {R} requests, each client one "
-                               f"conversation alternating /handle-agent-utterance and /handle-customer-utterance "
-                               f"(config-2 utterances), werkzeug threaded server, MicroBatcher(max_batch=1024, "
-                               f"max_wait={args.batch_wait_ms:g} ms)", "clients": C,
+        "config": {"workload": f"{C} HTTP/1.1 keep-alive clients in {n_proc} spawned processes on 127.0.0.1 x {R} "
+                               f"requests, each client one conversation alternating /handle-agent-utterance and "
+                               f"/handle-customer-utterance (config-2 utterances), werkzeug threaded server, "
+                               f"MicroBatcher(max_batch=1024, max_wait={args.batch_wait_ms:g} ms)", "clients": C,
                    "batch_wait_ms": args.batch_wait_ms},
         "latency_ms": {"p50": round(float(np.percentile(all_lat, 50)), 3),
                        "p90": round(float(np.percentile(all_lat, 90)), 3),
                        "p99": round(float(np.percentile(all_lat, 99)), 3), "max": round(float(all_lat[-1]), 3)},
-        "transcript_MBps": round(sum(nbytes) / el / 1e6, 3),
-        "errors": int(sum(errors)),
+        "transcript_MBps": round(nbytes / el / 1e6, 3),
+        "errors": int(errors),
         "micro_batches": {"count": int(len(sizes)), "mean_size": round(float(sizes.mean()), 2) if len(sizes) else 0,
                           "max_size": int(sizes.max()) if len(sizes) else 0},
         "process_requests_direct_per_s": round(direct, 1),
