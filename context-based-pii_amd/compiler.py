@@ -726,8 +726,11 @@ class Rules:
                 pat = r"(?i)\b(?:" + "|".join(re.escape(w) for w in words) + r")\b"
             else:
                 raise RuleError(f"unsupported custom infoType {name}")
+            # dictionary words: a 3-character prefix fires at most word starts of ordinary text (13x the
+            # matches on config 5's text), a 4-character one about 1.5x (SCAN prefilter, see plan_scan_groups)
             self.patterns.append(Pattern(len(self.patterns), name, pat,
-                                         lik_value(c.get("likelihood", "VERY_LIKELY")), None, True))
+                                         lik_value(c.get("likelihood", "VERY_LIKELY")), None, True,
+                                         DICT_SCAN_PREFIX if "dictionary" in c else None))
         for p in self.patterns:
             if p.validator not in VALIDATOR_IDS:
                 raise RuleError(f"unknown validator {p.validator}")
@@ -866,12 +869,20 @@ def _acc_tables(m: MealyDFA):
 
 SCAN_LDS_BYTES = 65536          # k_scan tables: u16 LDS byte addresses (class map + D rows + K rows)
 SCAN_CMAP_BYTES = 1024
-SCAN_GROUP_BYTES = 62 * 1024    # D table of a scan group >= 1 (its K is a 1-row never-accepting stub)
+SCAN_GROUP_BYTES = 62 * 1024    # D table of a scan group >= 1 that keeps 16-bit byte addresses (two
+                                # k_scan workgroups per CU); its K is a 1-row never-accepting stub
+SCAN_WIDE_BYTES = 124 * 1024    # a WIDE group >= 1 (engine: rows padded to 4 entries, entries = offset / 2,
+                                # one workgroup per CU): up to 64k transitions
 SCAN_GROUPS_MAX = 8             # k_pairs merges at most this many per-group event lists per lane
+DICT_SCAN_PREFIX = 4            # SCAN prefix of dictionary infoTypes (Rules)
 
 
 def _table_bytes(m: MealyDFA) -> int:
     return m.n_states * ((m.n_classes + 2) & ~1) * 2
+
+
+def _table_bytes_wide(m: MealyDFA) -> int:
+    return m.n_states * ((m.n_classes + 4) & ~3) * 2
 
 
 def _scan_dfa(patterns: Sequence[Pattern], budget: int, max_bytes: Optional[int] = None,
@@ -927,13 +938,28 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
         raise RuleError("the built-in detectors' SCAN automaton does not fit k_scan's LDS")
     out = [(base, g0)]
 
+    def fits(m, wide):
+        return m is not None and (_table_bytes(m) <= SCAN_GROUP_BYTES or
+                                  (wide and _table_bytes_wide(m) <= SCAN_WIDE_BYTES and
+                                   m.n_states * ((m.n_classes + 4) & ~3) <= 65536))
+
     def split(pats):
-        m = _scan_dfa_fit(pats, budget, SCAN_GROUP_BYTES)
-        if m is not None:
+        # the declared prefixes (dictionary types: DICT_SCAN_PREFIX) are worth a split -- they cut the
+        # candidate pairs several-fold -- so a set is halved before its prefixes are shortened, and a
+        # set with declared prefixes may take a WIDE table (one k_scan workgroup per CU); a set without
+        # them is halved until it fits the narrow limit (two workgroups per CU).  A single pattern whose
+        # automaton does not fit falls back to `budget` characters.
+        wide = any(p.scan_prefix for p in pats)
+        m = _scan_dfa(pats, budget, SCAN_WIDE_BYTES if wide else SCAN_GROUP_BYTES)
+        if fits(m, wide):
             out.append((pats, m))
             return
         if len(pats) == 1:
-            raise RuleError(f"the SCAN automaton of {pats[0].type_name} alone does not fit k_scan's LDS")
+            m = _scan_dfa(pats, budget, SCAN_WIDE_BYTES, prefixes=False)
+            if not fits(m, True):
+                raise RuleError(f"the SCAN automaton of {pats[0].type_name} alone does not fit k_scan's LDS")
+            out.append((pats, m))
+            return
         h = len(pats) // 2
         split(pats[:h])
         split(pats[h:])

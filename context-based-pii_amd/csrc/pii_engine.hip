@@ -65,7 +65,10 @@ struct Event {
 struct RulesDev {
     int P, G, T, V, SD, CD, d_start, SK, CK, k_start, n_hot, min_len;
     int kw_always_min, NE;
-    int CDs, CKs;                // row strides of the SCAN tables (CD / CK rounded up to even)
+    int CDs, CKs;                // row strides of the SCAN tables (CD / CK rounded up to even; a WIDE
+                                 // group's D: to a multiple of 4)
+    int dsh;                     // D entry = row byte offset >> dsh (| flags): 0, or 1 for a WIDE SCAN
+                                 // group >= 1 (D table up to 128 KiB; its class words carry no K half)
     uint32_t n_dacc, n_kacc;     // D / K accept sets
     const uint32_t* cmap4;    // [256] 2*classD | 2*classK << 16 (byte offsets)
     const uint16_t* td;       // [SD*CDs] LDS byte address of the next row in k_scan | accept (bit 0)
@@ -399,8 +402,8 @@ __device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* _
     uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
     for (int64_t b = (int64_t)top - 1; b >= (int64_t)L.hi; --b) {
         const uint32_t x = R.cmap4[tb[b]];
-        const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
-        const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
+        const uint32_t ad = ((nd & ~pm & 0xfffcu) << R.dsh) + (x & 0xffffu);
+        const uint32_t ak = (nk & ~pm & 0xfffcu) + (R.SK > 1 ? (x >> 16) : tk_base);   // (groups >= 1: K stub)
         nd = R.td[(ad - SCAN_TD_BASE) >> 1];
         nk = R.tk[(ak - tk_base) >> 1];
         pm = 0;
@@ -522,7 +525,7 @@ __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t j) {
 __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, uint32_t& cnt, uint32_t m,
                                            const uint32_t (&ad)[8], const uint32_t (&ak)[8], uint32_t p0,
                                            uint32_t lo_r, uint32_t len_r, uint32_t tk_base, uint32_t eot_d,
-                                           uint32_t eot_k) {
+                                           uint32_t eot_k, uint32_t dsh) {
     do {
         const uint32_t b = (uint32_t)__builtin_ctz(m);
         m &= m - 1u;
@@ -530,7 +533,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, 
         uint32_t a = sel8(ad, j), k = sel8(ak, j);
         uint32_t pos = p0 + j + 1u;
         if (b & 1u) {
-            a = (lds_u16(a) & 0xfffcu) + eot_d;
+            a = ((lds_u16(a) & 0xfffcu) << dsh) + eot_d;
             k = (lds_u16(k) & 0xfffcu) + eot_k;
             pos -= 1u;
         }
@@ -548,7 +551,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, 
 // then keeps an end-of-text accept only on a byte that starts an utterance.
 #define SCAN_STEP8(J, H)                                                                          \
     {                                                                                             \
-        ad[J] = (nd & ~pm & 0xfffcu) + (cc[J] & 0xffffu);                                         \
+        ad[J] = HK ? (nd & ~pm & 0xfffcu) + (cc[J] & 0xffffu) : ((nd & ~pm & 0xfffcu) << dsh) + cc[J];  \
         ak[J] = HK ? (nk & ~pm & 0xfffcu) + (cc[J] >> 16) : tk_base;                              \
         nd = lds_u16(ad[J]);                                                                      \
         if (HK) nk = lds_u16(ak[J]);                                                              \
@@ -565,7 +568,7 @@ __device__ __forceinline__ void scan_emit8(Event* __restrict__ ev, uint32_t ab, 
         SCAN_STEP8(3, H) SCAN_STEP8(2, H) SCAN_STEP8(1, H) SCAN_STEP8(0, H)                       \
         m = (m >> 16) & mk;                                                                       \
         if (__builtin_expect(m != 0, 0))                                                          \
-            scan_emit8(ev, ab, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k); \
+            scan_emit8(ev, ab, cnt, m, ad, ak, bpos + (OFF) + (H), lo_r, len_r, tk_base, eot_d, eot_k, dsh); \
     }
 
 #define SCAN_SUB(W, OFF)                                                                          \
@@ -587,8 +590,11 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 
 // HK = false: a SCAN group >= 1, whose K is the never-accepting one-row stub -- K is not stepped (its
 // row stays the start row, its transition is the stub's class-0 entry), one LDS read less per byte
-template <bool HK>
-__global__ __launch_bounds__(SCAN_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+// NT: 768 threads (two workgroups per CU with tables <= 80 KiB, 6 waves / SIMD), or SCAN_BLOCK_WIDE for
+// a WIDE group's table (one workgroup per CU: 16 waves instead of 12)
+constexpr int SCAN_BLOCK_WIDE = 1024;
+template <bool HK, int NT = SCAN_BLOCK>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? 6 : 4, NT == SCAN_BLOCK ? 6 : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
@@ -627,6 +633,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 6
         const uint32_t ab = (uint32_t)ev_base(L, c);
         const uint32_t eot_d = SCAN_TD_BASE + 2u * (uint32_t)(R.CD - 1), eot_k = tk_base + 2u * (uint32_t)(R.CK - 1);
         const uint32_t spread = tk_base + (uint32_t)nk_words * 4;     // scan_spread table (after K)
+        const uint32_t dsh = HK ? 0u : (uint32_t)R.dsh;               // (group 0 is never wide)
         // "previous byte started an utterance": start rows; a lane cut at hi continues from its halo state
         uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
         if (L.chi) {
@@ -701,8 +708,8 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
     for (int64_t b = (int64_t)L.hi - 1; b >= (int64_t)L.lo; --b) {
         const uint32_t cls = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)(4u * tb[b]));
         const uint32_t x = cls;
-        const uint32_t ad = (nd & ~pm & 0xfffcu) + (x & 0xffffu);
-        const uint32_t ak = (nk & ~pm & 0xfffcu) + (x >> 16);
+        const uint32_t ad = ((nd & ~pm & 0xfffcu) << R.dsh) + (x & 0xffffu);
+        const uint32_t ak = (nk & ~pm & 0xfffcu) + (R.SK > 1 ? (x >> 16) : tk_base);
         nd = lds_u16(ad);
         nk = lds_u16(ak);
         const bool st = v >= vmin && g_off(g, (uint32_t)v) == b;
@@ -710,8 +717,8 @@ __device__ void rescan_lane(const RulesDev& R, const Geo& g, const uint8_t* __re
         if ((nd | nk) & 1u) scan_emit(ev, ab, cnt, (uint32_t)b + 1u, lo_r, len_r, ad, ak, tk_base);
         if (st) {
             if ((nd | nk) & 2u)
-                scan_emit(ev, ab, cnt, (uint32_t)b, lo_r, len_r, (nd & 0xfffcu) + eot_d, (nk & 0xfffcu) + eot_k,
-                          tk_base);
+                scan_emit(ev, ab, cnt, (uint32_t)b, lo_r, len_r, ((nd & 0xfffcu) << R.dsh) + eot_d,
+                          (nk & 0xfffcu) + eot_k, tk_base);
             --v;
             while (v >= vmin && g_off(g, (uint32_t)v + 1) == g_off(g, (uint32_t)v)) --v;     // empty rows
         }
@@ -4238,8 +4245,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(Rq, g, text, e->lane_pos,
                                                                      q == 0 ? e->bnd : nullptr, stq);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
-                (q == 0 ? k_scan<true> : k_scan<false>)<<<(n_chunks + SCAN_BLOCK - 1) / SCAN_BLOCK, SCAN_BLOCK,
-                                                            e->sg_lds[q], st>>>(
+                const int nt = Rq.dsh ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
+                (q == 0 ? k_scan<true> : Rq.dsh ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
+                    (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], st>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
                 if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
                 if (e->long_min != NO_CUTS)
@@ -4667,6 +4675,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     // an entry is free for the destination's end-of-text accept
     R.CDs = (R.CD + 1) & ~1;
     R.CKs = (R.CK + 1) & ~1;
+    R.dsh = 0;
     const uint32_t td_words = (uint32_t)(R.SD * R.CDs / 2), tk_words = (uint32_t)(R.SK * R.CKs / 2);
     const uint32_t tk_base = SCAN_TD_BASE + td_words * 4;
     if ((uint64_t)tk_base + (uint64_t)tk_words * 4 > 65536) return fail("SCAN tables exceed 64 KiB of LDS");
@@ -4697,13 +4706,13 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     // destination row's byte offset from the table base, so a reset is "row 0"; the class words carry
     // the table bases; accept-id tables follow the same placement)
     auto relayout = [](const uint16_t* s, const uint16_t* acc, int S, int C, int Cs, int start, uint16_t* t,
-                       uint16_t* a) {
+                       uint16_t* a, int dsh = 0) {
         auto pos = [start](uint32_t r) { return r == (uint32_t)start ? 0u : r == 0 ? (uint32_t)start : r; };
         for (int r = 0; r < S; ++r)
             for (int c = 0; c < C; ++c) {
                 const uint32_t v = s[r * C + c], dst = v & 0x7fff;
                 const uint32_t eot = s[dst * C + C - 1] >> 15;
-                t[pos(r) * Cs + c] = (uint16_t)((pos(dst) * Cs * 2) | (v >> 15) | (eot << 1));
+                t[pos(r) * Cs + c] = (uint16_t)(((pos(dst) * Cs * 2) >> dsh) | (v >> 15) | (eot << 1));
                 a[pos(r) * Cs + c] = acc[r * C + c];
             }
     };
@@ -4764,7 +4773,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     tok.append(32, '\0');     // k_redact reads aligned 16-byte windows past a token's end
     // SCAN groups >= 1: their own D automaton and class map, a 1-row never-accepting K stub
     struct HostGroup {
-        int SD, CD, CDs, start;
+        int SD, CD, CDs, start, dsh;
         uint32_t lds;
         std::vector<uint16_t> td, tk, dacc, kacc, npair;
         std::vector<uint32_t> cmap4;
@@ -4784,21 +4793,31 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             h.SD = (int)gm[0];
             h.CD = (int)gm[1];
             h.CDs = (h.CD + 1) & ~1;
+            h.dsh = 0;
             if (!sc || !st || !sa || st->bytes != (size_t)h.SD * h.CD * 2 || sa->bytes != st->bytes || sc->bytes != 256)
                 return fail("SCAN group tables malformed");
+            // a table past 64 KiB of LDS addresses is WIDE: rows padded to a multiple of 4 entries (8-byte
+            // aligned), entries hold the row offset / 2, so 16-bit entries reach 128 KiB (and the u16
+            // transition index of an event, 64k entries)
+            if (SCAN_TD_BASE + (size_t)h.SD * h.CDs * 2 + 4 + SCAN_SPREAD_BYTES > 65536) {
+                h.CDs = (h.CD + 3) & ~3;
+                h.dsh = 1;
+                if ((size_t)h.SD * h.CDs > 65536) return fail("a SCAN group exceeds 128 KiB of LDS");
+            }
             const uint32_t tkb = SCAN_TD_BASE + (uint32_t)(h.SD * h.CDs) * 2;
             h.lds = tkb + 4 + SCAN_SPREAD_BYTES;                // + the K stub's row (2 entries), spread masks
-            if (h.lds > 65536) return fail("a SCAN group exceeds 64 KiB of LDS");
+            if (h.lds + FIX_LDS > 160 * 1024) return fail("a SCAN group exceeds the LDS");
             h.td.assign((size_t)h.SD * h.CDs, 0);
             h.dacc.assign((size_t)h.SD * h.CDs, 0);
             if (gm[2] < 0 || gm[2] >= h.SD) return fail("SCAN group start state out of range");
             relayout(reinterpret_cast<const uint16_t*>(st->data), reinterpret_cast<const uint16_t*>(sa->data), h.SD,
-                     h.CD, h.CDs, (int)gm[2], h.td.data(), h.dacc.data());
+                     h.CD, h.CDs, (int)gm[2], h.td.data(), h.dacc.data(), h.dsh);
             h.tk = {0, 0};
             h.kacc = {0, 0};
             h.start = 0;
             h.cmap4.resize(256);
-            for (int b = 0; b < 256; ++b) h.cmap4[b] = (SCAN_TD_BASE + 2u * sc->data[b]) | tkb << 16;   // K stub: class 0
+            // class words of a group >= 1: the D half only (its K is the stub, stepped at tk_base)
+            for (int b = 0; b < 256; ++b) h.cmap4[b] = SCAN_TD_BASE + 2u * sc->data[b];
             hg.push_back(std::move(h));
         }
     }
@@ -4977,6 +4996,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         Rq.SD = h.SD;
         Rq.CD = h.CD;
         Rq.CDs = h.CDs;
+        Rq.dsh = h.dsh;
         Rq.d_start = h.start;
         Rq.SK = 1;
         Rq.CK = 2;
@@ -4992,7 +5012,9 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         (hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
          hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
-             hipSuccess))
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan<false, SCAN_BLOCK_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)max_lds) != hipSuccess))
         return fail("cannot raise LDS limit");
     if (max_lds + FIX_LDS > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize,
