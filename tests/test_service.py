@@ -533,7 +533,7 @@ def test_service_maps_engine_nomem_and_capacity_to_processing_error(oracle_cfg):
     import torch
     from oracle import pii_oracle as O
     S, E = pkg("service"), pkg("engine")
-    svc = S.PiiService(n_slots=1024, clock=Clock(), time_base="payload")     # (no slot eviction below)
+    svc = S.PiiService(n_slots=4096, clock=Clock(), time_base="payload")     # (1300 conversations below: no slot eviction)
     eng = svc.engine
     small = [{"conversation_id": "s", "participant_role": "AGENT", "text": "What is your email address?",
               "start_timestamp_usec": 1}]
