@@ -2565,9 +2565,6 @@ struct RSpan {          // one kept span in batch order (16 B)
     uint32_t in_hi;
 };
 
-#ifndef REDACT_U
-#define REDACT_U 2
-#endif
 // Output assembly shared by k_redact and k_win_redact.  The piece table (s_pout = tile-relative
 // output offset of each piece, s_psrc = ABSOLUTE device address of its first byte; a sentinel
 // s_pout[total_p] = tile output length) is in LDS; a block -> piece table is built, then lane i
@@ -2617,87 +2614,55 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
     if (total_p == 0) return;
     uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
     const int64_t span = out_hi - out_lo;
-    // REDACT_U blocks per lane and iteration: the blocks that lie inside one piece (all but the few
-    // that hold a token boundary or a tile / row edge) have their loads issued together before any
-    // store, so a lane keeps REDACT_U load pairs in flight instead of one
-    for (int64_t q0 = q_lo + tid; q0 <= q_hi; q0 += (int64_t)REDACT_U * REDACT_BLOCK) {
-        uint4 v[REDACT_U];
-        uint32_t pis[REDACT_U];
-        bool fast[REDACT_U];
-#pragma unroll
-        for (int u = 0; u < REDACT_U; ++u) {
-            const int64_t q = q0 + (int64_t)u * REDACT_BLOCK;
-            v[u] = make_uint4(0, 0, 0, 0);
-            fast[u] = false;
-            pis[u] = 0;
-            if (q > q_hi) continue;
-            const int64_t r0 = q * 16 - omis - out_lo;
-            uint32_t pi;
-            if (table) {
-                pi = s_bp[q - q_lo];
-            } else {
-                const uint32_t rs = (uint32_t)(r0 < 0 ? 0 : r0);
-                uint32_t lo_i = 0, hi_i = total_p - 1;   // last piece with s_pout <= rs
-                while (lo_i < hi_i) {
-                    const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-                    if (s_pout[mid] <= rs) lo_i = mid;
-                    else hi_i = mid - 1;
-                }
-                pi = lo_i;
+    for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
+        const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
+        const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
+        const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
+        uint32_t pi;
+        if (table) {
+            pi = s_bp[q - q_lo];
+        } else {
+            const uint32_t rs = (uint32_t)(r0 + b_lo);
+            uint32_t lo_i = 0, hi_i = total_p - 1;       // last piece with s_pout <= rs
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                if (s_pout[mid] <= rs) lo_i = mid;
+                else hi_i = mid - 1;
             }
-            pis[u] = pi;
-            const int64_t qs = s_pout[pi], qe = s_pout[pi + 1];
-            if (r0 >= 0 && r0 + 16 <= span && qs <= r0 && qe >= r0 + 16) {
-                fast[u] = true;
-                v[u] = load16(reinterpret_cast<const uint8_t*>(s_psrc[pi]) + (r0 - qs), 0, 16);
-            }
+            pi = lo_i;
         }
-#pragma unroll
-        for (int u = 0; u < REDACT_U; ++u) {
-            const int64_t q = q0 + (int64_t)u * REDACT_BLOCK;
-            if (q > q_hi || fast[u]) continue;
-            const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
-            const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
-            const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
-            uint32_t pi = pis[u];
-            uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
-            uint64_t qsrc = s_psrc[pi];
-            uint4 w4 = make_uint4(0, 0, 0, 0);
-            for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
-                const int lo = max(b_lo, (int)((int64_t)qs - r0));
-                const int hi = min(b_hi, (int)((int64_t)qe - r0));
-                if (hi > lo) {
-                    const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
-                    const uint4 w = load16(reinterpret_cast<const uint8_t*>(qsrc) + delta, lo, hi);
-                    w4.x |= w.x & (bytemask(hi) & ~bytemask(lo));
-                    w4.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
-                    w4.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
-                    w4.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
+        uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
+        uint64_t qsrc = s_psrc[pi];
+        uint4 v = make_uint4(0, 0, 0, 0);
+        for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
+            const int lo = max(b_lo, (int)((int64_t)qs - r0));
+            const int hi = min(b_hi, (int)((int64_t)qe - r0));
+            if (hi > lo) {
+                const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
+                const uint4 w = load16(reinterpret_cast<const uint8_t*>(qsrc) + delta, lo, hi);
+                if (lo == 0 && hi == 16) {
+                    v = w;
+                } else {
+                    v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
+                    v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
+                    v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
+                    v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
                 }
-                if ((int64_t)qe >= r0 + b_hi) break;
-                ++pi;
-                qs = qe;
-                qe = s_pout[pi + 1];
-                qsrc = s_psrc[pi];
             }
-            v[u] = w4;
+            if ((int64_t)qe >= r0 + b_hi) break;
+            ++pi;
+            qs = qe;
+            qe = s_pout[pi + 1];
+            qsrc = s_psrc[pi];
         }
+        if (b_lo == 0 && b_hi == 16) {
+            op[q] = v;
+        } else {
+            uint8_t* ob = out - omis + q * 16;
+            const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int u = 0; u < REDACT_U; ++u) {
-            const int64_t q = q0 + (int64_t)u * REDACT_BLOCK;
-            if (q > q_hi) continue;
-            const int64_t r0 = q * 16 - omis - out_lo;
-            const int b_lo = r0 < 0 ? (int)-r0 : 0;
-            const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
-            if (b_lo == 0 && b_hi == 16) {
-                op[q] = v[u];
-            } else {
-                uint8_t* ob = out - omis + q * 16;
-                const uint32_t vw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
-            }
+            for (int j = 0; j < 16; ++j)
+                if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
         }
     }
 }
