@@ -350,6 +350,42 @@ struct FirstState {
     int last;   // end of the last match seen, -1 none
 };
 
+// byte K of a 16-byte window
+template <int K>
+__device__ __forceinline__ uint32_t wbyte(const uint4& w) {
+    const uint32_t x = (K & 8) ? ((K & 4) ? w.w : w.z) : ((K & 4) ? w.y : w.x);
+    return (x >> ((K & 3) * 8)) & 0xffu;
+}
+// byte classes of bytes H .. H + 7 of a window, issued together before the steps that use them (a
+// class does not depend on the automaton state, so a step waits on one LDS read instead of two)
+template <int H>
+__device__ __forceinline__ void classes8(const uint8_t* cm, const uint4& w, uint32_t (&cl)[8]) {
+    cl[0] = cm[wbyte<H + 0>(w)];
+    cl[1] = cm[wbyte<H + 1>(w)];
+    cl[2] = cm[wbyte<H + 2>(w)];
+    cl[3] = cm[wbyte<H + 3>(w)];
+    cl[4] = cm[wbyte<H + 4>(w)];
+    cl[5] = cm[wbyte<H + 5>(w)];
+    cl[6] = cm[wbyte<H + 6>(w)];
+    cl[7] = cm[wbyte<H + 7>(w)];
+}
+
+// FIRST steps over the first n (<= 8) bytes whose classes are cl, byte 0 at text position p0:
+// false = the run ended (r holds its result in `last`)
+__device__ __forceinline__ bool first_steps8(const uint16_t* tr, uint32_t nc, const uint32_t (&cl)[8], int n,
+                                             int p0, uint32_t& st, int& last) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (k < n) {
+            const uint32_t e = tr[st * nc + cl[k]];
+            st = e & DFA_STATE_MASK;
+            if (e & 0x4000u) last = p0 + k;
+            if (e & 0x8000u) return false;
+        }
+    }
+    return true;
+}
+
 __device__ __forceinline__ int first_finish(const Pool& pool, const int32_t* d, const uint8_t* text, int L,
                                             FirstState& r) {
     const uint16_t* tr = pool.trans + d[0];
@@ -357,13 +393,17 @@ __device__ __forceinline__ int first_finish(const Pool& pool, const int32_t* d, 
     const uint32_t nc = (uint32_t)d[3];
     uint32_t st = r.st;
     int last = r.last;
-    const int lo = r.pos;
-    PII_FOR_BYTES(text, lo, L, {
-        const uint32_t e = tr[st * nc + cm[c]];
-        st = e & DFA_STATE_MASK;
-        if (e & 0x4000u) last = lo + i;
-        if (e & 0x8000u) return last;
-    })
+    for (int j = r.pos; j < L; j += 16) {
+        const int n = L - j < 16 ? L - j : 16;
+        const uint4 w = load16(text + j, 0, n);
+        uint32_t cl[8];
+        classes8<0>(cm, w, cl);
+        if (!first_steps8(tr, nc, cl, n, j, st, last)) return last;
+        if (n > 8) {
+            classes8<8>(cm, w, cl);
+            if (!first_steps8(tr, nc, cl, n - 8, j + 8, st, last)) return last;
+        }
+    }
     if (tr[st * nc + nc - 1] & 0x4000u) last = L;
     return last;
 }
@@ -380,7 +420,6 @@ __device__ __forceinline__ int first_begin(const Pool& pool, const int32_t* d, c
     const int hi = L - lo < FIRST_WINDOW ? L : lo + FIRST_WINDOW;
     uint4 w = load16(text + lo, 0, hi - lo > 0 ? hi - lo : 1);
     uint32_t st;
-    int j = s;
     if (s == 0) {
         st = (uint32_t)d[4];
     } else {
@@ -388,19 +427,22 @@ __device__ __forceinline__ int first_begin(const Pool& pool, const int32_t* d, c
         shr8(w);
     }
     int last = -1;
-    for (; j < hi; ++j) {
-        const uint32_t e = tr[st * nc + cm[w.x & 0xffu]];
-        st = e & DFA_STATE_MASK;
-        if (e & 0x4000u) last = j;
-        if (e & 0x8000u) return last;
-        shr8(w);
+    const int n = hi - s;
+    if (n > 0) {
+        uint32_t cl[8];
+        classes8<0>(cm, w, cl);
+        if (!first_steps8(tr, nc, cl, n, s, st, last)) return last;
+        if (n > 8) {
+            classes8<8>(cm, w, cl);
+            if (!first_steps8(tr, nc, cl, n - 8, s + 8, st, last)) return last;
+        }
     }
-    if (j >= L) {
+    if (hi >= L) {
         if (tr[st * nc + nc - 1] & 0x4000u) last = L;
         return last;
     }
     r.st = st;
-    r.pos = j;
+    r.pos = hi;
     r.last = last;
     return -2;
 }
@@ -411,17 +453,34 @@ __device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, con
     return e != -2 ? e : first_finish(pool, d, text, L, r);
 }
 
-// Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics)
+// Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics).
+// Four bytes' classes are read together before their steps (a class does not depend on the state,
+// so a step waits on one LDS read instead of two); a runtime loop over the 4-byte groups keeps the
+// unrolled part (and k_pair_eval's registers) small.
 __device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
     const uint16_t* tr = pool.trans + d[0];
     const uint8_t* cm = pool.cmap + d[2];
     const uint32_t nc = (uint32_t)d[3];
     uint32_t st = (uint32_t)d[4];
-    PII_FOR_BYTES(text, lo, hi, {
-        const uint32_t e = tr[st * nc + cm[c]];
-        if (e & 0x4000u) return true;
-        st = e & DFA_STATE_MASK;
-    })
+    for (int j = lo; j < hi; j += 16) {
+        const int n = hi - j < 16 ? hi - j : 16;
+        uint4 w = load16(text + j, 0, n);
+#pragma unroll 1
+        for (int g = 0; g < n; g += 4) {
+            const uint32_t x = w.x;
+            const uint32_t c0 = cm[x & 0xffu], c1 = cm[(x >> 8) & 0xffu], c2 = cm[(x >> 16) & 0xffu], c3 = cm[x >> 24];
+            const uint32_t cl[4] = {c0, c1, c2, c3};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (g + k < n) {
+                    const uint32_t e = tr[st * nc + cl[k]];
+                    if (e & 0x4000u) return true;
+                    st = e & DFA_STATE_MASK;
+                }
+            }
+            w = make_uint4(w.y, w.z, w.w, 0u);
+        }
+    }
     return (tr[st * nc + nc - 1] & 0x4000u) != 0;
 }
 
