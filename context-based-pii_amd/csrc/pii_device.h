@@ -456,12 +456,10 @@ __device__ __forceinline__ int first_run(const Pool& pool, const int32_t* d, con
 // Unanchored HOT DFA over text[lo, hi) with the window edges as text edges (re.search semantics).
 // Four bytes' classes are read together before their steps (a class does not depend on the state,
 // so a step waits on one LDS read instead of two); a runtime loop over the 4-byte groups keeps the
-// unrolled part (and k_pair_eval's registers) small.
-__device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
-    const uint16_t* tr = pool.trans + d[0];
-    const uint8_t* cm = pool.cmap + d[2];
-    const uint32_t nc = (uint32_t)d[3];
-    uint32_t st = (uint32_t)d[4];
+// unrolled part (and k_pair_eval's registers) small.  hot_span steps text[lo, hi) from state st:
+// true = an accept.
+__device__ __forceinline__ bool hot_span(const uint16_t* tr, const uint8_t* cm, uint32_t nc, const uint8_t* text,
+                                         int lo, int hi, uint32_t& st) {
     for (int j = lo; j < hi; j += 16) {
         const int n = hi - j < 16 ? hi - j : 16;
         uint4 w = load16(text + j, 0, n);
@@ -481,6 +479,15 @@ __device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, cons
             w = make_uint4(w.y, w.z, w.w, 0u);
         }
     }
+    return false;
+}
+
+__device__ __forceinline__ bool hot_run(const Pool& pool, const int32_t* d, const uint8_t* text, int lo, int hi) {
+    const uint16_t* tr = pool.trans + d[0];
+    const uint8_t* cm = pool.cmap + d[2];
+    const uint32_t nc = (uint32_t)d[3];
+    uint32_t st = (uint32_t)d[4];
+    if (hot_span(tr, cm, nc, text, lo, hi, st)) return true;
     return (tr[st * nc + nc - 1] & 0x4000u) != 0;
 }
 

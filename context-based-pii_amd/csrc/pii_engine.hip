@@ -318,27 +318,6 @@ __device__ __forceinline__ uint32_t lane_bucket(const Geo& g, uint32_t c) {
 
 constexpr uint32_t LANE_SORT_CHUNK = 1024;         // lanes per workgroup (4 per thread; ~1k workgroups at config 2)
 
-// LDS counter add aggregated over the wavefront: the lanes holding the same bucket add once (most
-// lanes of a batch share a length bucket, and same-address LDS atomics serialise); returns each
-// active lane's rank among the wavefront's lanes of its bucket, added to the counter's old value
-__device__ __forceinline__ uint32_t wave_bucket_add(uint32_t* h, uint32_t bk, bool act) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1;
-    uint64_t todo = __ballot(act);
-    uint32_t rank = 0;
-    while (todo) {
-        const int leader = __ffsll((unsigned long long)todo) - 1;
-        const uint32_t lb = __shfl(bk, leader);
-        const uint64_t same = __ballot(act && bk == lb);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&h[lb], (uint32_t)__popcll(same));
-        base = __shfl(base, leader);
-        if (act && bk == lb) rank = base + (uint32_t)__popcll(same & below);
-        todo &= ~same;
-    }
-    return rank;
-}
-
 // also records every lane's geometry (g.lanes is null here; later kernels read the records)
 __global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __restrict__ bucket_cnt,
                                                     uint4* __restrict__ lanes) {
@@ -346,16 +325,12 @@ __global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __res
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
     __syncthreads();
     const uint32_t c0 = blockIdx.x * LANE_SORT_CHUNK, c1 = min(c0 + LANE_SORT_CHUNK, g.n_chunks);
-    for (uint32_t c = c0 + threadIdx.x; c < c0 + LANE_SORT_CHUNK; c += blockDim.x) {
-        const bool act = c < c1;
-        uint32_t bk = 0;
-        if (act) {
-            const Lane L = g_lane_slow(g, c);
-            lanes[c] = lane_pack(L);
-            const uint32_t len = L.hi - min(L.lo, L.hi);
-            bk = (uint32_t)(LANE_NB - 1) - min(len >> 5, (uint32_t)(LANE_NB - 1));
-        }
-        (void)wave_bucket_add(h, bk, act);
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+        const Lane L = g_lane_slow(g, c);
+        lanes[c] = lane_pack(L);
+        const uint32_t len = L.hi - min(L.lo, L.hi);
+        const uint32_t bk = (uint32_t)(LANE_NB - 1) - min(len >> 5, (uint32_t)(LANE_NB - 1));
+        atomicAdd(&h[bk], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
@@ -388,7 +363,7 @@ __global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __res
     for (int j = 0; j < PER; ++j) {
         const uint32_t c = c0 + j * 256 + threadIdx.x;
         bk[j] = c < g.n_chunks ? lane_bucket(g, c) : 0u;
-        rk[j] = wave_bucket_add(h, bk[j], c < g.n_chunks);
+        rk[j] = c < g.n_chunks ? atomicAdd(&h[bk[j]], 1u) : 0u;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x)
@@ -3064,12 +3039,7 @@ __device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WinRing& W
         if (sh >= lo) {
             if (sl >= hi) break;
             const int a = (int)(max(lo, sl) - sl), b = (int)(min(hi, sh) - sl);
-            const uint8_t* t = Ej.t;
-            PII_FOR_BYTES(t, a, b, {
-                const uint32_t x = tr[st * nc + cm[c]];
-                if (x & 0x4000u) return true;
-                st = x & DFA_STATE_MASK;
-            })
+            if (hot_span(tr, cm, nc, Ej.t, a, b, st)) return true;
             if (j + 1 < it.nw && sh < hi) {
                 const uint32_t x = tr[st * nc + cm['\n']];
                 if (x & 0x4000u) return true;
