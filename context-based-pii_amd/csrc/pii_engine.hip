@@ -4378,8 +4378,14 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->tev[3], st));
-    if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
-    if ((rc = exclusive_scan(e, e->lane_nf, n_chunks, e->lane_sp, st))) return rc;
+    // row output offsets and per-lane span offsets: one dual scan for a big batch (3 launches instead
+    // of 6), two single-pass look-back scans for a small one
+    if (n_chunks > 0 && (n_utt + LB_TILE - 1) / LB_TILE > LB_MAX_TILES) {
+        if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st, e->lane_nf, n_chunks, e->lane_sp))) return rc;
+    } else {
+        if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
+        if ((rc = exclusive_scan(e, e->lane_nf, n_chunks, e->lane_sp, st))) return rc;
+    }
     k_finalize<<<1, 1, 0, st>>>(out_offs, e->lane_sp, n_utt, n_chunks, out_cap, span_cap, e->d_err, e->d_totals,
                                 pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, nullptr);
     HIPCHK(hipGetLastError());
