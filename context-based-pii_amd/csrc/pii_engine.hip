@@ -1441,22 +1441,40 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
         }
     }
     uint32_t run = 0;                                     // lane: pairs of its events handled so far
-    for (uint32_t f0 = 0; f0 < total; f0 += 64) {
-        const uint32_t f = f0 + lane;
-        const bool act = f < total;
-        int ow = 0;                                       // owner: first lane with incl > f
+    // event f's owner (first lane with incl > f) and record; the next chunk's are loaded while this
+    // chunk is processed (one dependent load less per chunk)
+    auto owner_of = [&](uint32_t f) {
+        int ow = 0;
 #pragma unroll
         for (int step = 32; step >= 1; step >>= 1) {
             const uint32_t v = __shfl(incl, ow + step - 1);
             if (v <= f) ow += step;
         }
+        return ow;
+    };
+    auto event_of = [&](uint32_t f, int ow) {
         const uint32_t o_ex = __shfl(excl, ow), o_eb = __shfl(eb, ow);
+        Event E{};
+        if (f < total) E = ev[(uint64_t)o_eb + (f - o_ex)];
+        return E;
+    };
+    int ow_n = owner_of(lane);
+    Event E_n = event_of(lane, ow_n);
+    for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+        const uint32_t f = f0 + lane;
+        const bool act = f < total;
+        const int ow = ow_n;
+        const Event E = E_n;
+        if (f0 + 64 < total) {
+            ow_n = owner_of(f + 64);
+            E_n = event_of(f + 64, ow_n);
+        }
+        const uint32_t o_ex = __shfl(excl, ow);
         const uint32_t o_u0 = __shfl(u0, ow), o_u1 = __shfl(u1, ow), o_run = __shfl(run, ow);
         const uint64_t o_top = WRITE ? __shfl(top, ow) : 0;
-        Event E{};
+        (void)o_ex;
         uint32_t n = 0, acc = 0, u = 0, kg = (uint32_t)KW_NONE;
         if (act) {
-            E = ev[(uint64_t)o_eb + (f - o_ex)];
             n = npair[E.sd];
             if (WRITE) acc = R.d_accid[E.sd];
             else if (q == 0) kg = R.k_grp[E.sk];
