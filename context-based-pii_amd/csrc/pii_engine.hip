@@ -3727,13 +3727,24 @@ __global__ __launch_bounds__(256) void k_win_join(const WinRing W, const WinBatc
     }
 }
 
-// the counter block a second pass over the same call starts from: the first pass's error flags
-// (minus a queue overflow of its pair queue, whose pairs are not used) and its context commit count
+// the counter block a second pass over the same call starts from: the first pass's error flags and its
+// context commit count.  The first pass writes no pair queue (launch_front with pair_first = false), so
+// an ERR_QUEUE here is a real overflow: it is kept, with the queue needs, so that every stage of pass 2
+// bails out and pii_sync grows the queues and re-runs the call.
 __global__ void k_err_save(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ saved) {
-    saved[0] = cnt[0] & ~(uint32_t)ERR_QUEUE;
+    saved[0] = cnt[0];
     saved[1] = 0;
     saved[2] = cnt[2];
-    saved[3] = saved[4] = saved[5] = 0;
+    saved[3] = cnt[3];
+    saved[4] = cnt[4];
+    saved[5] = cnt[5];
+}
+
+// the totals of a context-only call (pii_context_update): no output, no spans, its error flags
+__global__ void k_ctx_totals(const uint32_t* __restrict__ err, uint64_t* __restrict__ totals) {
+    totals[0] = totals[1] = 0;
+    totals[2] = *err;
+    totals[3] = totals[4] = totals[5] = 0;
 }
 
 __global__ void k_noop() {}
@@ -4281,7 +4292,10 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             if ((rc = exclusive_scan(e, e->lane_np, n_chunks, e->lane_pair, st, multi ? e->lane_evn : e->lane_cnt,
                                      n_chunks, e->lane_ev)))
                 return rc;
-            if (multi) {
+            // (no pair queue when no FIRST runs follow: the first pass of a full window re-scan and a
+            // context-only call need the keyword groups of the count pass only, and cannot overflow it)
+            if (!pair_first) {
+            } else if (multi) {
                 k_pairs<true, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
                                                                  e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
                                                                  e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
@@ -4466,6 +4480,34 @@ int ensure_window_scratch(pii_engine* e, uint32_t n_utt) {
     return PII_OK;
 }
 
+// the window history rings (pii_window_enable, pii_context_resize): persistent per-slot state, plain
+// allocations outside the work-buffer accounting; empty rings
+struct WinTables {
+    WDesc* desc = nullptr;
+    uint32_t *cnt = nullptr, *head = nullptr;
+    uint8_t* arena = nullptr;
+};
+int alloc_window_tables(pii_engine* e, WinTables& w, size_t ns, uint32_t window_n, uint32_t slot_bytes) {
+    const bool ok = hipMalloc(&w.desc, ns * window_n * sizeof(WDesc)) == hipSuccess &&
+                    hipMalloc(&w.cnt, ns * 4) == hipSuccess && hipMalloc(&w.head, ns * 4) == hipSuccess &&
+                    hipMalloc(&w.arena, ns * (size_t)slot_bytes) == hipSuccess &&
+                    hipMemset(w.cnt, 0, ns * 4) == hipSuccess && hipMemset(w.head, 0, ns * 4) == hipSuccess;
+    if (ok) return PII_OK;
+    for (void* p : {(void*)w.desc, (void*)w.cnt, (void*)w.head, (void*)w.arena})
+        if (p) (void)hipFree(p);
+    w = WinTables{};
+    (void)hipGetLastError();
+    e->err = "device allocation failed: the window history rings";
+    return PII_E_NOMEM;
+}
+void free_window_tables(pii_engine* e) {
+    for (void* p : {(void*)e->wr_desc, (void*)e->wr_cnt, (void*)e->wr_head, (void*)e->wr_arena})
+        if (p) (void)hipFree(p);
+    e->wr_desc = nullptr;
+    e->wr_cnt = e->wr_head = nullptr;
+    e->wr_arena = nullptr;
+}
+
 int ensure_join(pii_engine* e, uint32_t n_utt) {
     int rc;
     if (n_utt + 1 > e->cap_j_utt) {
@@ -4622,8 +4664,48 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     return PII_OK;
 }
 
+// pii_context_update: the shared front without the pair queue or FIRST runs (the count pass yields the
+// AGENT rows' keyword groups), the context kernels and the context commit
+int run_context(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_t n_utt, uint64_t total_bytes,
+                const uint32_t* slot, const uint8_t* role, const int64_t* ts, int16_t* ctx_info, hipStream_t st) {
+    if (total_bytes > PII_MAX_BATCH_BYTES || total_bytes + 2ull * n_utt + (total_bytes >> MIN_LANE_SHIFT) > 0xFFFFFFF0ull) {
+        e->err = "batch larger than PII_MAX_BATCH_BYTES (positions and event arenas are 32-bit); split it";
+        return PII_E_ARG;
+    }
+    e->lane_shift = pick_lane_shift(e, total_bytes);
+    e->r0 = (uint32_t)((uintptr_t)text & 63);
+    e->long_min = 2u << e->lane_shift;
+    const uint32_t n_chunks = lane_count(e, total_bytes);
+    e->last_lanes = n_chunks;
+    int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
+    if (rc) return rc;
+    e->last = pii_engine::Call{text, offs, n_utt, 0, total_bytes, slot, role, ts, nullptr, 0, nullptr, nullptr,
+                               0, ctx_info, st, nullptr, nullptr, 0};
+    e->last_kind = 2;
+    e->kev_valid = false;
+    const unsigned long long* pcount =
+        n_chunks > 0 ? reinterpret_cast<const unsigned long long*>(e->lane_pair + n_chunks) : e->pair_count;
+    if ((rc = launch_front(e, text, offs, n_utt, n_chunks, 0, total_bytes, slot, role, ts, ctx_info, nullptr, pcount,
+                           st, nullptr, true, false)))
+        return rc;
+    HIPCHK(hipEventRecord(e->tev[3], st));
+    k_ctx_totals<<<1, 1, 0, st>>>(e->d_err, e->d_totals);
+    HIPCHK(hipEventRecord(e->tev[4], st));
+    if (n_utt > 0)
+        k_ctx_commit<<<std::min<uint32_t>((n_utt + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
+            slot, e->kw, ts, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->tev[5], st));
+    HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 64, hipMemcpyDeviceToHost, st));
+    e->h_hist_valid = false;
+    HIPCHK(hipEventRecord(e->tev[6], st));
+    return PII_OK;
+}
+
 int rerun_last(pii_engine* e) {
     const pii_engine::Call c = e->last;
+    if (e->last_kind == 2)
+        return run_context(e, c.text, c.offs, c.n_utt, c.total, c.slot, c.role, c.ts, c.ctx_info, c.st);
     if (e->last_kind == 1)
         return run_window(e, c.text, c.offs, c.n_utt, c.base, c.total, c.slot, c.role, c.ts, c.out, c.out_cap,
                           c.out_offs, c.spans, c.span_cap, c.ctx_info, c.st);
@@ -5348,6 +5430,46 @@ int host_call(pii_engine* e, bool window, const uint8_t* bytes, const uint64_t* 
     return PII_OK;
 }
 
+// pii_context_update: stage the rows as host_call does, run the context-only pipeline, copy ctx_info back
+int host_context(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                 const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, int16_t* ctx_info) {
+    if (!e || !offsets || (n_utt && (!conv_slot || !role))) return PII_E_ARG;
+    for (uint32_t i = 0; i < n_utt; ++i)
+        if (offsets[i + 1] < offsets[i]) return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    const uint64_t base = offsets[0], total = offsets[n_utt] - base;
+    int rc;
+    if (total + 16 > e->cap_h_bytes) {
+        const uint64_t nb = total + total / 8 + 64;
+        if ((rc = grow(e, e->h_text, nb))) return rc;
+        e->cap_h_bytes = nb;
+    }
+    if (n_utt + 1 > e->cap_h_utt) {
+        const uint32_t nu = n_utt + n_utt / 8 + 64;
+        if ((rc = grow(e, e->h_offs, nu + 1)) || (rc = grow(e, e->h_out_offs, nu + 1)) ||
+            (rc = grow(e, e->h_slot, nu)) || (rc = grow(e, e->h_role, nu)) || (rc = grow(e, e->h_ts, nu)) ||
+            (rc = grow(e, e->h_ctx, nu)))
+            return rc;
+        e->cap_h_utt = nu;
+    }
+    hipStream_t st = e->stream;
+    std::vector<uint64_t> rel(n_utt + 1);
+    for (uint32_t i = 0; i <= n_utt; ++i) rel[i] = offsets[i] - base;
+    if (total) HIPCHK(hipMemcpyAsync(e->h_text, bytes + base, total, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->h_offs, rel.data(), (n_utt + 1) * 8, hipMemcpyHostToDevice, st));
+    if (n_utt) {
+        HIPCHK(hipMemcpyAsync(e->h_slot, conv_slot, n_utt * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->h_role, role, n_utt, hipMemcpyHostToDevice, st));
+        if (ts_us) HIPCHK(hipMemcpyAsync(e->h_ts, ts_us, n_utt * 8, hipMemcpyHostToDevice, st));
+    }
+    if ((rc = run_context(e, e->h_text, e->h_offs, n_utt, total, e->h_slot, e->h_role, ts_us ? e->h_ts : nullptr,
+                          e->h_ctx, st)))
+        return rc;
+    if ((rc = pii_sync(e, nullptr))) return rc;
+    if (ctx_info && n_utt) HIPCHK(hipMemcpy(ctx_info, e->h_ctx, n_utt * 2, hipMemcpyDeviceToHost));
+    return PII_OK;
+}
+
 int device_call(pii_engine* e, bool window, const uint8_t* d_bytes, const uint64_t* d_offsets, uint32_t n_utt,
                 const uint32_t* d_slot, const uint8_t* d_role, const int64_t* d_ts, uint8_t* d_out, uint64_t out_cap,
                 uint64_t* d_out_offsets, pii_span* d_spans, uint32_t span_cap, int16_t* d_ctx_info, void* stream,
@@ -5385,6 +5507,11 @@ int pii_scan_redact(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets
                      span_cap, n_spans, ctx_info);
 }
 
+int pii_context_update(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                       const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, int16_t* ctx_info) {
+    return host_context(e, bytes, offsets, n_utt, conv_slot, role, ts_us, ctx_info);
+}
+
 int pii_scan_redact_ext(pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
                         const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, uint8_t* out_bytes,
                         uint64_t out_cap, uint64_t* out_offsets, pii_span* spans, uint32_t span_cap, uint32_t* n_spans,
@@ -5410,21 +5537,91 @@ int pii_window_enable_ex(pii_engine* e, uint32_t window_n, uint32_t slot_bytes, 
     if (!e || window_n == 0 || window_n > WN_MAX || slot_bytes < 64 || slot_bytes % 16 ||
         (flags & ~(uint32_t)PII_WINDOW_FULL))
         return PII_E_ARG;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    // the history rings are persistent state like the context table (not work buffers: they do not
+    // count against pii_set_scratch_limit); a failed allocation leaves the previous window, if any,
+    // enabled and unchanged
+    const size_t ns = std::max<uint32_t>(1, e->n_slots);
+    WinTables w;
+    int rc = alloc_window_tables(e, w, ns, window_n, slot_bytes);
+    if (rc) return rc;
+    free_window_tables(e);
+    e->wr_desc = w.desc;
+    e->wr_cnt = w.cnt;
+    e->wr_head = w.head;
+    e->wr_arena = w.arena;
     // the incremental path needs: no detector that consumes '\n' or tests a text edge (a match inside a
     // window is then its utterance's own match), at most P_MAX patterns, one SCAN group, LDS-resident
     // tables; any other rule set re-scans the joined windows in full
     e->win_full = (flags & PII_WINDOW_FULL) || !e->window_ok || e->R.P > P_MAX || e->n_sg > 1 || !e->wsel_ok;
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    const size_t ns = std::max<uint32_t>(1, e->n_slots);
-    int rc;
-    if ((rc = grow(e, e->wr_desc, ns * window_n)) || (rc = grow(e, e->wr_cnt, ns)) || (rc = grow(e, e->wr_head, ns)) ||
-        (rc = grow(e, e->wr_arena, ns * (size_t)slot_bytes)))
-        return rc;
-    HIPCHK(hipMemset(e->wr_cnt, 0, ns * 4));
-    HIPCHK(hipMemset(e->wr_head, 0, ns * 4));
     e->win_n = window_n;
     e->win_slot_bytes = slot_bytes;
+    return PII_OK;
+}
+
+int pii_context_resize(pii_engine* e, uint32_t n_conv_slots) {
+    if (!e || n_conv_slots < e->n_slots) return PII_E_ARG;
+    if (n_conv_slots == e->n_slots) return PII_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const size_t ns = n_conv_slots, old = std::max<uint32_t>(1, e->n_slots);
+    int32_t* g = nullptr;
+    int64_t* t = nullptr;
+    uint32_t* s = nullptr;
+    auto undo = [&](int rc) {
+        if (g) (void)hipFree(g);
+        if (t) (void)hipFree(t);
+        if (s) (void)hipFree(s);
+        (void)hipGetLastError();
+        e->err = "device allocation failed: the context table could not grow";
+        return rc;
+    };
+    if (hipMalloc(&g, ns * 4) != hipSuccess || hipMalloc(&t, ns * 8) != hipSuccess || hipMalloc(&s, ns * 4) != hipSuccess)
+        return undo(PII_E_NOMEM);
+    WinTables w;
+    if (e->win_n) {
+        const int rc = alloc_window_tables(e, w, ns, e->win_n, e->win_slot_bytes);
+        if (rc) return undo(rc);
+    }
+    // new slots: no context record, no window history; old slots keep theirs (slot-major layouts)
+    std::vector<int32_t> none(ns - old, -1);
+    bool ok = hipMemcpy(g, e->st_group, old * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
+              hipMemcpy(g + old, none.data(), (ns - old) * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(t, e->st_ts, old * 8, hipMemcpyDeviceToDevice) == hipSuccess &&
+              hipMemset(t + old, 0, (ns - old) * 8) == hipSuccess &&
+              hipMemcpy(s, e->stamp, old * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
+              hipMemset(s + old, 0, (ns - old) * 4) == hipSuccess;
+    if (ok && e->win_n) {
+        const size_t N = e->win_n, sb = e->win_slot_bytes;
+        ok = hipMemcpy(w.desc, e->wr_desc, old * N * sizeof(WDesc), hipMemcpyDeviceToDevice) == hipSuccess &&
+             hipMemcpy(w.cnt, e->wr_cnt, old * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
+             hipMemcpy(w.head, e->wr_head, old * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
+             hipMemcpy(w.arena, e->wr_arena, old * sb, hipMemcpyDeviceToDevice) == hipSuccess;
+    }
+    if (!ok) {
+        if (e->win_n) {
+            (void)hipFree(w.desc);
+            (void)hipFree(w.cnt);
+            (void)hipFree(w.head);
+            (void)hipFree(w.arena);
+        }
+        return undo(PII_E_DEVICE);
+    }
+    (void)hipFree(e->st_group);
+    (void)hipFree(e->st_ts);
+    (void)hipFree(e->stamp);
+    e->st_group = g;
+    e->st_ts = t;
+    e->stamp = s;
+    if (e->win_n) {
+        free_window_tables(e);
+        e->wr_desc = w.desc;
+        e->wr_cnt = w.cnt;
+        e->wr_head = w.head;
+        e->wr_arena = w.arena;
+    }
+    e->n_slots = n_conv_slots;
     return PII_OK;
 }
 

@@ -27,7 +27,8 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_last_timings_ex", "pii_last_queue_sizes", "pii_last_stats", "pii_window_enable", "pii_window_reset",
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
            "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext", "pii_window_enable_ex",
-           "pii_window_mode", "pii_set_scratch_limit", "pii_scratch_bytes"]
+           "pii_window_mode", "pii_set_scratch_limit", "pii_scratch_bytes", "pii_context_resize",
+           "pii_context_update"]
 PII_WINDOW_FULL = 1
 
 
@@ -91,6 +92,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_sync.argtypes = [P, U64]
     lib.pii_context_get.argtypes = [P, c.c_uint32, I32, I64]
     lib.pii_context_set.argtypes = [P, c.c_uint32, c.c_int32, c.c_int64]
+    lib.pii_context_resize.argtypes = [P, c.c_uint32]
+    lib.pii_context_update.argtypes = [P, P, P, c.c_uint32, P, P, P, P]
     lib.pii_histogram.argtypes = [P, U64, c.c_uint32]
     lib.pii_histogram_reset.argtypes = [P]
     lib.pii_last_timings.argtypes = [P, c.POINTER(c.c_float)]
@@ -384,6 +387,30 @@ class Engine:
         rc = self.lib.pii_context_set(self.h, slot, group, ts_us)
         if rc != PII_OK:
             raise self._err(rc, "pii_context_set")
+
+    def context_resize(self, n_slots: int) -> None:
+        """grow the conversation table to n_slots (pii_context_resize): live records and window
+        histories are kept, the new slots start empty"""
+        rc = self.lib.pii_context_resize(self.h, int(n_slots))
+        if rc != PII_OK:
+            raise self._err(rc, "pii_context_resize")
+        self.n_slots = int(n_slots)
+
+    def context_update(self, texts: Sequence[bytes], conv_slot: Sequence[int], role: Sequence[int],
+                       ts_us: Optional[Sequence[int]] = None) -> np.ndarray:
+        """The context half of scan_redact alone (pii_context_update): AGENT rows' keyword hits are
+        committed as scan_redact would; returns ctx_info (int16 per row)."""
+        data, offs = pack(texts)
+        n = len(texts)
+        slot = np.ascontiguousarray(conv_slot, dtype=np.uint32)
+        rl = np.ascontiguousarray(role, dtype=np.uint8)
+        ts = None if ts_us is None else np.ascontiguousarray(ts_us, dtype=np.int64)
+        ctx = np.empty(n, dtype=np.int16)
+        rc = self.lib.pii_context_update(self.h, _ptr(data) if len(data) else None, _ptr(offs), n, _ptr(slot),
+                                         _ptr(rl), _ptr(ts), _ptr(ctx))
+        if rc != PII_OK:
+            raise self._err(rc, "pii_context_update")
+        return ctx
 
     def histogram(self) -> np.ndarray:
         n = len(self.type_names)

@@ -15,7 +15,8 @@ this module keeps their names, argument meaning, return shapes and error behavio
 * ``redact_utterance_realtime(data)``              main.py:427-466 -- ({redacted_utterance}, 200):
   agent transcript + "\\n" + utterance, redacted with the context, last line kept.
 
-Conversation ids map onto engine context slots (``SlotMap``, least-recently-used reuse).  The agent
+Conversation ids map onto engine context slots (``SlotMap``): a slot is reused only once its
+conversation's record has expired (Redis TTL semantics), otherwise the engine's table grows.  The agent
 transcript of the last keyword hit -- the record's ``agent_transcript`` field -- is host data (only
 the realtime handler reads it) and lives beside the slot map; its expiry follows the engine's TTL.
 
@@ -23,8 +24,9 @@ Throughput path: ``process_batch`` runs many rows in one engine call (the batch 
 include/pii_engine.h: a conversation's rows contiguous and in entry order), and
 ``process_requests`` runs a micro-batch of concurrent handler requests in one engine call with the
 same results as calling the handlers one after another (``app.py`` is the Flask front end that
-coalesces concurrent HTTP requests into such micro-batches).  A batch with more conversations than
-the slot table holds is cut into runs that fit, so slot reuse never mixes two conversations.
+coalesces concurrent HTTP requests into such micro-batches).  A failed engine call (its rows get
+the reference's ``[DLP_*_ERROR]`` strings) still stores the agent rows' context, as the reference
+does after a failed DLP call.
 
 Stream formats: ``process_pubsub_batch`` takes the raw Pub/Sub utterance
 payloads (``{conversation_id, original_entry_index, participant_role, text, user_id,
@@ -48,6 +50,8 @@ import threading
 import time
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
 
 from .engine import (PII_E_ARG, PII_E_CAPACITY, PII_E_DEVICE, PII_E_NOMEM, PII_E_ORDER, PII_E_RULES,
                      ROLE_AGENT, ROLE_CUSTOMER, ROLE_OTHER, Engine, PiiError)
@@ -78,17 +82,30 @@ def _dec(b: bytes) -> str:
 
 
 class SlotMap:
-    """conversation_id -> engine context slot; slot 0 is reserved for stateless calls.  When all
-    slots are taken the least recently used conversation that is not pinned (part of the batch
-    being built) is evicted (its context is cleared)."""
+    """conversation_id -> engine context slot (the Redis key ``context:{conversation_id}`` -> its HBM
+    record); slot 0 is reserved for stateless calls.
 
-    def __init__(self, n_slots: int, on_evict: Optional[Callable[[int], None]] = None):
+    Redis keeps a key until its TTL runs out (main.py:163, 366-374), so a slot is reused only when
+    nothing the reference would still read lives in it: the conversation stored no context record,
+    or its record has expired (``now - ts >= ttl``, the engine's validity rule), and it has no
+    window history (the aggregator keeps a conversation's utterances until it ends).  Among those,
+    the least recently used conversation that is not pinned (part of the batch being built) goes
+    first; its slot is cleared (``on_evict``).  When no slot can be reused the table GROWS
+    (``on_grow(n)``, pii_context_resize: live records are kept), so a live context is never dropped."""
+
+    SCAN = 64            # LRU entries examined for a reusable slot before the table grows instead
+
+    def __init__(self, n_slots: int, on_evict: Optional[Callable[[int], None]] = None,
+                 on_grow: Optional[Callable[[int], None]] = None):
         if n_slots < 3:
             raise ValueError("need at least 3 slots (slot 0 is reserved)")
         self.n_slots = n_slots
         self.on_evict = on_evict
+        self.on_grow = on_grow
         self._map: "OrderedDict[object, int]" = OrderedDict()
         self._free = list(range(n_slots - 1, 0, -1))
+        self.live_until: Dict[int, int] = {}      # slot -> time its context record expires (us)
+        self.windowed: set = set()                 # slots holding window history
 
     @property
     def capacity(self) -> int:
@@ -97,22 +114,57 @@ class SlotMap:
     def __len__(self):
         return len(self._map)
 
-    def get(self, conversation_id, pinned: Optional[set] = None) -> int:
+    def note_context(self, slot: int, until_us: int) -> None:
+        """a context record was stored in `slot`, valid until `until_us` (ts + ttl)"""
+        self.live_until[slot] = max(self.live_until.get(slot, until_us), until_us)
+
+    def note_window(self, slot: int) -> None:
+        self.windowed.add(slot)
+
+    def reusable(self, slot: int, now_us: Optional[int]) -> bool:
+        if slot in self.windowed:
+            return False
+        until = self.live_until.get(slot)
+        return until is None or (now_us is not None and now_us >= until)
+
+    def _forget(self, slot: int) -> None:
+        self.live_until.pop(slot, None)
+        self.windowed.discard(slot)
+
+    def get(self, conversation_id, pinned: Optional[set] = None, now_us: Optional[int] = None) -> int:
         s = self._map.get(conversation_id)
         if s is not None:
             self._map.move_to_end(conversation_id)
             return s
-        if self._free:
-            s = self._free.pop()
-        else:
-            victim = next((c for c in self._map if not pinned or c not in pinned), None)
-            if victim is None:
-                raise RuntimeError("every slot is pinned by the current batch")
-            s = self._map.pop(victim)
-            if self.on_evict:
-                self.on_evict(s)
+        if not self._free:
+            victim, seen = None, 0
+            for c, cs in self._map.items():
+                if pinned and c in pinned:
+                    continue
+                if self.reusable(cs, now_us):
+                    victim = c
+                    break
+                seen += 1
+                if seen >= self.SCAN:
+                    break
+            if victim is not None:
+                s = self._map.pop(victim)
+                self._forget(s)
+                if self.on_evict:
+                    self.on_evict(s)
+                self._map[conversation_id] = s
+                return s
+            self._grow()
+        s = self._free.pop()
         self._map[conversation_id] = s
         return s
+
+    def _grow(self) -> None:
+        n = self.n_slots * 2
+        if self.on_grow:
+            self.on_grow(n)                       # raises if the device cannot hold the larger table
+        self._free = list(range(n - 1, self.n_slots - 1, -1)) + self._free
+        self.n_slots = n
 
     def peek(self, conversation_id) -> Optional[int]:
         return self._map.get(conversation_id)
@@ -120,6 +172,7 @@ class SlotMap:
     def release(self, conversation_id) -> Optional[int]:
         s = self._map.pop(conversation_id, None)
         if s is not None:
+            self._forget(s)
             self._free.append(s)
         return s
 
@@ -155,7 +208,7 @@ class PiiService:
         self.time_base = time_base
         self._payload_now: Optional[int] = None
         self.lock = threading.Lock()
-        self.slots = SlotMap(self.engine.n_slots, on_evict=self._evict)
+        self.slots = SlotMap(self.engine.n_slots, on_evict=self._evict, on_grow=self.engine.context_resize)
         self.group_of_type: Dict[str, int] = {}
         for g, t in enumerate(self.engine.group_types):
             self.group_of_type.setdefault(t, g)
@@ -207,19 +260,41 @@ class PiiService:
         return self.engine.scan_redact(texts, slots, roles, ts, ext=ext)
 
     def _sub_batches(self, keys: Sequence[object], split_before: Optional[Sequence[bool]] = None) -> List[List[int]]:
-        """Row indices cut into runs whose distinct-conversation count fits the slot table (so
-        assigning slots for one run never evicts a conversation of the same run)."""
-        cap = self.slots.capacity - 1
-        out, cur, seen = [], [], set()
-        for i, k in enumerate(keys):
-            if cur and ((k not in seen and len(seen) >= cap) or (split_before and split_before[i])):
+        """Row indices cut into runs at the marked rows (the slot table grows instead of evicting a
+        live conversation, so a run may hold any number of conversations)."""
+        out, cur = [], []
+        for i in range(len(keys)):
+            if cur and split_before and split_before[i]:
                 out.append(cur)
-                cur, seen = [], set()
+                cur = []
             cur.append(i)
-            seen.add(k)
         if cur:
             out.append(cur)
         return out
+
+    def _note(self, slots, roles, texts, ts, ctx_info) -> None:
+        """After an engine call (or its context-only fallback): AGENT rows whose keyword hit stored a
+        context record -- the Redis SETEX of main.py:366-374, with the record's agent_transcript."""
+        for k, (sl, r) in enumerate(zip(slots, roles)):
+            if r == ROLE_AGENT and int(ctx_info[k]) >= 0:
+                self.agent_text[sl] = (texts[k], ts[k])
+                self.slots.note_context(sl, ts[k] + self.ttl_us)
+
+    def _context_fallback(self, texts: Sequence[bytes], slots, roles, ts) -> np.ndarray:
+        """After a failed engine call: the context half alone (pii_context_update), so AGENT rows
+        still store their context, as the reference's extract_expected_pii + SETEX run after a
+        failed DLP call (call_dlp_for_redaction never raises, main.py:358-374).  A batch too big for
+        the engine's memory is halved until the parts fit (in row order: a conversation's context
+        flows from one part into the next).  ctx_info per row, -2 where the device could not run it."""
+        n = len(texts)
+        try:
+            return np.asarray(self.engine.context_update(texts, slots, roles, ts), dtype=np.int16)
+        except PiiError as e:
+            if e.code != PII_E_NOMEM or n <= 1:
+                return np.full(n, -2, np.int16)
+        h = n // 2
+        return np.concatenate([self._context_fallback(texts[:h], slots[:h], roles[:h], ts[:h]),
+                               self._context_fallback(texts[h:], slots[h:], roles[h:], ts[h:])])
 
     # ---------------------------------------------------------------- reference seam (main.py:580)
     def call_dlp_for_redaction(self, transcript: str, context: Optional[dict]) -> str:
@@ -303,16 +378,14 @@ class PiiService:
                 out[i] = err
             else:
                 valid.append(i)
-        split, agents, cur_convs = [], set(), set()
-        cap = self.slots.capacity - 1
+        split, agents = [], set()
         for i in valid:
             kind, data = reqs[i]
             cid = data["conversation_id"]
-            cut = (kind == "realtime" and cid in agents) or (cid not in cur_convs and len(cur_convs) >= cap)
+            cut = kind == "realtime" and cid in agents
             if cut:
-                agents, cur_convs = set(), set()
+                agents = set()
             split.append(cut)
-            cur_convs.add(cid)
             if kind == "agent":
                 agents.add(cid)
         for run in self._sub_batches([reqs[i][1]["conversation_id"] for i in valid], split):
@@ -338,7 +411,7 @@ class PiiService:
                     else:
                         rows.append((slot, i, utt, ROLE_CUSTOMER, False))
                 else:
-                    slot = self.slots.get(cid, pinned)
+                    slot = self.slots.get(cid, pinned, now)
                     rows.append((slot, i, data["transcript"], ROLE_AGENT if kind == "agent" else ROLE_CUSTOMER, False))
             # the batch contract: a slot's rows contiguous, in arrival order
             first: Dict[int, int] = {}
@@ -346,35 +419,41 @@ class PiiService:
                 first.setdefault(r[0], k)
             order = sorted(range(len(rows)), key=lambda k: (first[rows[k][0]], k))
             rows = [rows[k] for k in order]
+            texts = [_enc(r[2]) for r in rows]
+            slots, roles, ts = [r[0] for r in rows], [r[3] for r in rows], [now] * len(rows)
             try:
-                res = self._run([_enc(r[2]) for r in rows], [r[0] for r in rows], [r[3] for r in rows],
-                                [now] * len(rows))
+                res = self._run(texts, slots, roles, ts)
             except PiiError as e:
                 # The reference's handlers never fail on a DLP error: the error string is the transcript
-                # (main.py:752-773) and context_used reports the Redis GET (main.py:425).  The engine
-                # call is atomic, so a failed call stores no context (context_stored False).
-                for slot, i, text, role, split_last in rows:
+                # (main.py:752-773), the agent handler still extracts and stores the context
+                # (main.py:358-374) and context_used reports the Redis GET (main.py:425).  The engine
+                # call is atomic (nothing committed), so its context half runs again alone.
+                ctx = self._context_fallback(texts, slots, roles, ts)
+                self._note(slots, roles, [r[2] for r in rows], ts, ctx)
+                for k, (slot, i, text, role, split_last) in enumerate(rows):
                     kind, data = reqs[i]
+                    g = int(ctx[k])
                     if kind == "agent":
-                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_stored": False}, 200)
+                        out[i] = ({"redacted_transcript": error_string(e.code, text), "context_stored": g >= 0}, 200)
                     elif kind == "customer":
-                        try:
-                            used = self._context_record(slot, now) is not None
-                        except PiiError:
-                            used = False
+                        used = g >= 0
+                        if g == -2:
+                            try:
+                                used = self._context_record(slot, now) is not None
+                            except PiiError:
+                                used = False
                         out[i] = ({"redacted_transcript": error_string(e.code, text), "context_used": used}, 200)
                     else:                                   # main.py:458-461 on the error string
                         red = error_string(e.code, text)
                         lines = red.splitlines() if split_last else [red]
                         out[i] = ({"redacted_utterance": lines[-1] if lines else ""}, 200)
                 return
+            self._note(slots, roles, [r[2] for r in rows], ts, res.ctx_info)
             for k, (slot, i, text, role, split_last) in enumerate(rows):
                 kind, data = reqs[i]
                 red = _dec(res.text(k))
                 g = int(res.ctx_info[k])
                 if kind == "agent":
-                    if g >= 0:
-                        self.agent_text[slot] = (text, now)
                     out[i] = ({"redacted_transcript": red, "context_stored": g >= 0}, 200)
                 elif kind == "customer":
                     out[i] = ({"redacted_transcript": red, "context_used": g >= 0}, 200)
@@ -401,17 +480,21 @@ class PiiService:
                 part = [rows[i] for i in run]
                 pinned = {r["conversation_id"] for r in part}
                 texts = [_enc(r["text"]) for r in part]
-                slots = [self.slots.get(r["conversation_id"], pinned) for r in part]
-                roles = [role_code(r.get("participant_role")) for r in part]
                 ts = [self._row_ts(r, now) for r in part]
+                now = self._now_us()
+                slots = [self.slots.get(r["conversation_id"], pinned, now) for r in part]
+                roles = [role_code(r.get("participant_role")) for r in part]
                 try:
                     res = self.engine.rescan_window(texts, slots, roles, ts)
                 except PiiError as e:
+                    # the context is stored regardless (main.py:358-374); the rows do not enter the windows
+                    self._note(slots, roles, [r["text"] for r in part], ts,
+                               self._context_fallback(texts, slots, roles, ts))
                     out.extend(error_string(e.code, r["text"]) for r in part)
                     continue
-                for i, r in enumerate(part):
-                    if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
-                        self.agent_text[slots[i]] = (r["text"], ts[i])
+                for sl in slots:
+                    self.slots.note_window(sl)
+                self._note(slots, roles, [r["text"] for r in part], ts, res.ctx_info)
                 out.extend(_dec(res.text(i)) for i in range(len(part)))
         return out
 
@@ -437,17 +520,19 @@ class PiiService:
                 part = [rows[i] for i in run]
                 pinned = {r["conversation_id"] for r in part}
                 texts = [_enc(r["text"]) for r in part]
-                slots = [self.slots.get(r["conversation_id"], pinned) for r in part]
-                roles = [role_code(r.get("participant_role")) for r in part]
                 ts = [self._row_ts(r, now) for r in part]
+                now = self._now_us()
+                slots = [self.slots.get(r["conversation_id"], pinned, now) for r in part]
+                roles = [role_code(r.get("participant_role")) for r in part]
                 try:
                     res = self._run(texts, slots, roles, ts)
                 except PiiError as e:
+                    # the agent rows' context is stored regardless (main.py:358-374)
+                    self._note(slots, roles, [r["text"] for r in part], ts,
+                               self._context_fallback(texts, slots, roles, ts))
                     out.extend(error_string(e.code, r["text"]) for r in part)
                     continue
-                for i, r in enumerate(part):
-                    if roles[i] == ROLE_AGENT and int(res.ctx_info[i]) >= 0:
-                        self.agent_text[slots[i]] = (r["text"], ts[i])
+                self._note(slots, roles, [r["text"] for r in part], ts, res.ctx_info)
                 out.extend(_dec(res.text(i)) for i in range(len(part)))
         return out
 

@@ -147,7 +147,8 @@ int pii_scan_redact_device_ext(struct pii_engine* e, const uint8_t* d_bytes, con
  * grow on overflow (pii_sync re-runs the batch) -- their need depends on the text, not its size. */
 int pii_reserve(struct pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint64_t max_out, uint32_t max_spans);
 /* Bound the device memory of the engine's per-call work buffers (queues, arenas, staging; not the rules
- * or the context / window tables), e.g. on a GPU shared with other work; 0 = no limit.  A call that
+ * or the persistent context / window tables, which pii_engine_create, pii_window_enable and
+ * pii_context_resize allocate outside it), e.g. on a GPU shared with other work; 0 = no limit.  A call that
  * would need more fails with PII_E_NOMEM and commits nothing (the service maps it to
  * "[DLP_PROCESSING_ERROR] {transcript}", main.py:770-773); buffers already held stay valid.
  * pii_scratch_bytes reports what the work buffers hold now. */
@@ -159,6 +160,20 @@ int pii_sync(struct pii_engine* e, uint64_t totals[3]);
 /* per-conversation context record (replaces redis GET/SETEX of context:{id}) */
 int pii_context_get(struct pii_engine* e, uint32_t slot, int32_t* group, int64_t* ts_us);
 int pii_context_set(struct pii_engine* e, uint32_t slot, int32_t group, int64_t ts_us);
+/* Grow the conversation table to n_conv_slots (>= the current count; PII_E_ARG otherwise).  Redis
+ * keeps every context:{id} key until its TTL runs out (main.py:163, 366-374), so the host slot map
+ * grows the table instead of evicting a conversation whose record is still live.  Records and
+ * window histories of the existing slots are kept; new slots start empty.  Synchronous.  On failure
+ * (PII_E_NOMEM) the table is unchanged. */
+int pii_context_resize(struct pii_engine* e, uint32_t n_conv_slots);
+/* The context half of pii_scan_redact alone, for rows whose redaction failed: the reference stores
+ * an agent utterance's context even when its DLP call failed (call_dlp_for_redaction never raises;
+ * extract_expected_pii + SETEX run after it, main.py:358-374).  Same batch contract and context
+ * semantics (AGENT rows' keyword hits are committed, ctx_info as in pii_scan_redact: an AGENT row's
+ * own group, else the record the row read); no findings, no output, no histogram.  Needs the scan's
+ * work buffers but no pair queue, so it fits where a full call may not. */
+int pii_context_update(struct pii_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint32_t n_utt,
+                       const uint32_t* conv_slot, const uint8_t* role, const int64_t* ts_us, int16_t* ctx_info);
 
 /* per-info-type counts of kept findings since the last reset (counts[n_types]); the multi-GPU
  * driver all-reduces these over RCCL.  Each call copies the counts to pinned host memory with its

