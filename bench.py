@@ -332,8 +332,9 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
     # first_utt pair, offsets pair, event count (24 B) + 8 B per event written
     scan_B = n_bytes + (n_bytes + 63) // 64 * 8 + 24 * n_lanes + 8 * n_events
     scan_GBps = scan_B / max(k_ms["k_scan"] / 1e3, 1e-12) / 1e9
-    # k_redact: input + output bytes, its offset/count reads, the span copy (read + write)
-    red_B = n_bytes + ob + 8 * (n + 1) * 3 + 4 * n + 32 * ns
+    # k_redact: what it moves -- the input bytes, the output bytes, one 16-B RSpan per kept span and
+    # the 4-B first-span index per 64 KiB output tile (no offsets / counts, it reads none)
+    red_B = n_bytes + ob + 16 * ns + 4 * ((ob >> 16) + 2)
     red_GBps = red_B / max(k_ms["k_redact"] / 1e3, 1e-12) / 1e9
     wl = getattr(args, "workload", "scan")
     traffic = measured_traffic("k_scan", n_bytes, wl)

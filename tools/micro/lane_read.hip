@@ -2,6 +2,9 @@
 // (a) per-lane contiguous ranges read right-to-left in aligned 64-byte blocks (one block prefetched)
 // (b) the same ranges read left-to-right
 // (c) a fully coalesced stream (lane i reads 16 B at i, i+64*16, ...)
+// (d) the same stream read 8 B and 4 B per lane (the record / queue loads of the sparse kernels)
+// Every kernel reads exactly `bytes` per launch: tools/pmc_traffic.py turns their FETCH_SIZE into one
+// correction factor per access pattern.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -55,6 +58,20 @@ __global__ __launch_bounds__(256) void k_coalesced(const uint4* __restrict__ p, 
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+template <class T>
+__device__ __forceinline__ void k_stream(const T* __restrict__ p, uint64_t n, uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        acc ^= (uint32_t)p[i] ^ (uint32_t)((uint64_t)p[i] >> 16);
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void k_stream8(const uint64_t* __restrict__ p, uint64_t n, uint32_t* __restrict__ out) {
+    k_stream<uint64_t>(p, n, out);
+}
+__global__ __launch_bounds__(256) void k_stream4(const uint32_t* __restrict__ p, uint64_t n, uint32_t* __restrict__ out) {
+    k_stream<uint32_t>(p, n, out);
+}
+
 int main() {
     const uint64_t bytes = 1200ull << 20;
     uint4* d;
@@ -93,5 +110,19 @@ int main() {
         if (it) best = ms < best ? ms : best;
     }
     printf("coalesced: %.3f ms  %.0f GB/s\n", best, bytes / best / 1e6);
+    for (int w : {8, 4}) {
+        best = 1e9;
+        for (int it = 0; it < 6; ++it) {
+            (void)hipEventRecord(a);
+            if (w == 8) k_stream8<<<256 * 8, 256>>>(reinterpret_cast<const uint64_t*>(d), bytes / 8, o);
+            else k_stream4<<<256 * 8, 256>>>(reinterpret_cast<const uint32_t*>(d), bytes / 4, o);
+            (void)hipEventRecord(b);
+            (void)hipEventSynchronize(b);
+            float ms;
+            (void)hipEventElapsedTime(&ms, a, b);
+            if (it) best = ms < best ? ms : best;
+        }
+        printf("stream %d B/lane: %.3f ms  %.0f GB/s\n", w, best, bytes / best / 1e6);
+    }
     return 0;
 }

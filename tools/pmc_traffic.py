@@ -4,9 +4,17 @@ kernel sources, or null).
 
 HBM bytes: FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (TCC EA request counters).  The guide
 (MI355X_MICROARCH.md, HBM section) says gfx950 FETCH_SIZE under-reports wide streaming reads by 2x and
-that other access shapes must be calibrated: the correction used here is measured on
-tools/micro/lane_read's k_lane_rev, which reads exactly 1200 MiB per dispatch in the k_scan pattern
-(per-lane 1 KiB ranges, right to left, 64-byte blocks).
+that other access shapes must be calibrated.  tools/micro/lane_read reads exactly 1200 MiB per
+dispatch in four patterns, and each gives its own correction (bytes read / FETCH_SIZE bytes):
+  lane_rev  k_lane_rev   per-lane 1 KiB ranges, right to left, 64-byte blocks (k_scan's text reads)
+  stream16  k_coalesced  16 B per lane, consecutive (k_redact's text reads and tile stores' sources)
+  stream8   k_stream8    8 B per lane (the scan events, pair records: the queue kernels' main loads)
+  stream4   k_stream4    4 B per lane (offsets / counts / per-lane scalars)
+Every engine kernel is assigned the pattern of its dominant read stream (KERNEL_PATTERN), and its
+hbm_bytes = FETCH_SIZE x that pattern's correction + WRITE_SIZE.  (one global factor,
+calibrated on k_scan's pattern, under-counted k_redact's coalesced stream.)  Where the bench line
+gives the work sizes, the kernel's algorithmic bytes and traffic / algorithmic ratio
+are stored beside it.
 
 LDS-array cycles (scan workloads): SQ_LDS_IDX_ACTIVE is converted to LDS-array cycles with the factor
 tools/micro/lds_calib measures on ds_read_b32 patterns of known cost (2 / 4 / 8 cycles per
@@ -25,6 +33,49 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ["context-based-pii_amd/csrc/pii_engine.hip", "context-based-pii_amd/csrc/pii_device.h"]
 CALIB_BYTES = 1200 * (1 << 20)
+CALIB_KERNELS = {"lane_rev": "k_lane_rev", "stream16": "k_coalesced", "stream8": "k_stream8", "stream4": "k_stream4"}
+# dominant read stream per engine kernel (name prefix); anything else: stream8
+KERNEL_PATTERN = {"k_scan": "lane_rev", "k_scan_fix": "lane_rev", "k_redact": "stream16", "k_win_redact": "stream16",
+                  "k_win_join": "stream16", "k_lane_bits": "stream8", "k_chunk_index": "stream8",
+                  "k_pairs_flat": "stream8", "k_pairs": "stream8", "k_expand": "stream8", "k_pair_first": "stream8",
+                  "k_pair_eval": "stream8", "k_select": "stream8", "k_spans": "stream8", "k_ctx_scan": "stream4",
+                  "k_ctx_apply": "stream4", "k_ctx_commit": "stream4", "k_lane_count": "stream4",
+                  "k_lane_place": "stream4", "k_scan_reduce": "stream4", "k_scan_apply": "stream4",
+                  "k_scan_blocks": "stream4", "k_scan_lb": "stream4", "k_tile_first": "stream8",
+                  "k_hist_reduce": "stream4"}
+
+
+def pattern_of(kernel):
+    base = kernel.split("<")[0]
+    return KERNEL_PATTERN.get(base, "stream8")
+
+
+def algorithmic_bytes(kernel, b):
+    """DESIGN.md §6 algorithmic bytes of one launch, from the bench line b (None if not derivable)"""
+    if not b or "queues_per_step_per_gpu" not in b:
+        return None
+    n_bytes = b["config"].get("bytes_per_gpu")
+    U = b["config"].get("utterances_per_gpu")
+    q = b["queues_per_step_per_gpu"]
+    E, P = q.get("scan_events", 0), q.get("candidate_pairs", 0)
+    S = b.get("spans_per_step_per_gpu", 0)
+    lanes = (n_bytes + 1023) // 1024
+    base = kernel.split("<")[0]
+    if base == "k_scan" and kernel.startswith("k_scan<true"):
+        return b.get("roofline", {}).get("algorithmic_bytes")
+    if base == "k_redact":
+        return b.get("roofline_redact", {}).get("algorithmic_bytes")
+    if base == "k_pairs_flat" and "<false" in kernel:
+        return 8 * E + 12 * lanes                                # events in; lane counts in, pair counts out
+    if base == "k_pairs_flat":
+        return 8 * E + 16 * E + 8 * P + 24 * lanes               # events in; EvLoc + pairs out
+    if base == "k_spans":
+        return 16 * S * 3 + 16 * lanes                           # findings in; API spans + RSpans out
+    if base == "k_lane_bits":
+        return 8 * ((n_bytes + 63) // 64) + 8 * U + 16 * lanes   # start words out; offsets + lanes in
+    if base == "k_chunk_index":
+        return 8 * (U + 1) + U + 4 * U + 4 * U                   # offsets + roles in; defaults out
+    return None
 
 
 def per_kernel(d, counter):
@@ -65,24 +116,36 @@ def main():
     fetch = per_kernel(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "write"), "WRITE_SIZE")
     calib = per_kernel(os.path.join(d, "calib"), "FETCH_SIZE")
-    rev = calib.get("k_lane_rev", [])
-    # lane_read launches k_lane_rev at 512/1024/2048 B per lane, 6 times each: all read CALIB_BYTES
-    corr = CALIB_BYTES / (sum(rev) / len(rev) * 1024) if rev else None
+    # every lane_read launch reads CALIB_BYTES (k_lane_rev at 512/1024/2048 B per lane, the streams)
+    corrs = {pat: (CALIB_BYTES / (mean(calib[k]) * 1024) if calib.get(k) else None)
+             for pat, k in CALIB_KERNELS.items()}
+    corr = corrs["lane_rev"]
     bench = [json.loads(l) for l in open(os.path.join(d, "fetch.log")) if l.startswith("{")]
     n_bytes = bench[-1]["config"].get("bytes_per_gpu", bench[-1]["config"].get("bytes_per_step")) if bench else None
     h = hashlib.sha256()
     for f in SOURCES:
         h.update(open(os.path.join(ROOT, f), "rb").read())
     res = {"workload": w, "source_digest": h.hexdigest()[:16], "bytes_per_gpu": n_bytes, "fetch_correction": corr,
-           "note": "hbm_bytes = FETCH_SIZE*1024*fetch_correction + WRITE_SIZE*1024, mean per dispatch",
+           "fetch_corrections": corrs,
+           "note": "hbm_bytes = FETCH_SIZE*1024*fetch_corrections[fetch_pattern] + WRITE_SIZE*1024, mean per "
+                   "dispatch; algorithmic_bytes per DESIGN.md section 6 from the bench line's work sizes",
            "kernels": {}}
+    b = bench[-1] if bench else None
     for k in sorted(set(fetch) | set(write)):
         if not k.startswith("k_"):
             continue
         f = mean(fetch.get(k, [0])) * 1024
         wr = mean(write.get(k, [0])) * 1024
-        res["kernels"][k] = {"fetch_reported_bytes": round(f), "write_bytes": round(wr),
-                             "hbm_bytes": round(f * (corr or 1.0) + wr) if corr else None}
+        pat = pattern_of(k)
+        c = corrs.get(pat)
+        e = {"fetch_reported_bytes": round(f), "write_bytes": round(wr), "fetch_pattern": pat,
+             "hbm_bytes": round(f * c + wr) if c else None}
+        ab = algorithmic_bytes(k, b)
+        if ab:
+            e["algorithmic_bytes"] = int(ab)
+            if e["hbm_bytes"]:
+                e["traffic_over_algorithmic"] = round(e["hbm_bytes"] / ab, 3)
+        res["kernels"][k] = e
     if os.path.isdir(os.path.join(d, "lds")):
         unit, per = lds_unit(d)
         idx = per_kernel(os.path.join(d, "lds"), "SQ_LDS_IDX_ACTIVE")
