@@ -66,11 +66,13 @@ def algorithmic_bytes(kernel, b):
     if base == "k_redact":
         return b.get("roofline_redact", {}).get("algorithmic_bytes")
     if base == "k_pairs_flat" and "<false" in kernel:
-        return 8 * E + 12 * lanes                                # events in; lane counts in, pair counts out
+        # events in; the wavefronts' row offsets + roles staged; lane counts in, pair counts out
+        return 8 * E + 8 * (U + 1) + U + 12 * lanes
     if base == "k_pairs_flat":
-        return 8 * E + 16 * E + 8 * P + 24 * lanes               # events in; EvLoc + pairs out
+        return 8 * E + 8 * (U + 1) + 16 * E + 8 * P + 24 * lanes   # events + row offsets in; EvLoc + pairs out
     if base == "k_spans":
-        return 16 * S * 3 + 16 * lanes                           # findings in; API spans + RSpans out
+        # findings in, each one's row input / output base; API spans + RSpans out
+        return 16 * S + 16 * S + 32 * S + 16 * lanes
     if base == "k_lane_bits":
         return 8 * ((n_bytes + 63) // 64) + 8 * U + 16 * lanes   # start words out; offsets + lanes in
     if base == "k_chunk_index":
