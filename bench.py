@@ -253,6 +253,33 @@ class DeviceBatch:
                                   self.ctx.data_ptr())
 
 
+def reduce_over_ranks(dist, dev, elapsed: float, local_hist: np.ndarray, sums=()):
+    """The timed region's cross-rank bookkeeping (the one data collective is the
+    histogram all_reduce): max-over-ranks wall time, the SUM of each per-rank quantity in `sums`, the
+    reduced u64[T+1] histogram (last slot = span total), and its check against an all_gather of every
+    rank's own counts.  One rank (dist None): the local values.  Returns (elapsed, sums, reduced,
+    verified)."""
+    import torch
+    T = len(local_hist) - 1
+    sums = [float(x) for x in sums]
+    if dist is None:
+        return elapsed, sums, local_hist.copy(), bool(local_hist[T] == local_hist[:T].sum())
+    world = dist.get_world_size()
+    t = torch.tensor([elapsed] + sums, dtype=torch.float64, device=dev)
+    dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+    if sums:
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+    # (clone: on a CPU device .to() would alias the caller's array, and all_reduce works in place)
+    h = torch.from_numpy(np.array(local_hist, dtype=np.int64)).to(dev).clone()
+    dist.all_reduce(h)                                    # RCCL over xGMI under nccl: per-infoType counts
+    reduced = h.cpu().numpy()
+    parts = [torch.zeros(T + 1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(np.array(local_hist, dtype=np.int64)).to(dev).clone())
+    want = np.sum([p.cpu().numpy() for p in parts], axis=0)
+    verified = bool((want == reduced).all() and reduced[T] == reduced[:T].sum())
+    return float(t[0].item()), [float(x) for x in t[1:].tolist()], reduced, verified
+
+
 def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None, bank=None):
     """One rank of the config-2 benchmark: shard -> W warmup steps -> K timed steps between barriers
     + device syncs -> max-over-ranks time.  A step = one scan+redact pass over the rank's resident
@@ -301,17 +328,9 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
         dist.barrier()
     _sync(dev)
     elapsed = time.perf_counter() - t0
-    reduced = local.copy()
-    verified = bool(local[T] == local[:T].sum())
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        reduced = hist.cpu().numpy()
-        parts = [torch.zeros(T + 1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(parts, torch.from_numpy(local).to(dev))
-        want = np.sum([p.cpu().numpy() for p in parts], axis=0)
-        verified = bool((want == reduced).all() and reduced[T] == reduced[:T].sum())
+    elapsed, _, reduced, verified = reduce_over_ranks(dist if world > 1 else None, dev, elapsed, local)
+    if world > 1:        # the last step's in-loop all_reduce agrees with the one after timing
+        verified = verified and bool((hist.cpu().numpy() == reduced).all())
     per_stage /= args.steps
     k_ms = {k: v / args.steps for k, v in k_ms.items()}
     n_pairs, n_events = eng.queue_sizes()
@@ -950,17 +969,9 @@ def stream_rank(args, rank, world, dev, eng, dist=None, cpu=None):
     local = np.zeros(T + 1, dtype=np.int64)
     local[:T] = eng.histogram().astype(np.int64)
     local[T] = st["spans"]
-    reduced, verified = local.copy(), bool(local[T] == local[:T].sum())
-    tot_in = st["bytes_in"]
-    if world > 1:
-        t = torch.tensor([elapsed, float(tot_in)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, tot_in = float(t[0].item()), int(t[1].item())
-        h = torch.from_numpy(local).to(dev)
-        dist.all_reduce(h)
-        reduced = h.cpu().numpy()
-        verified = bool(reduced[T] == reduced[:T].sum())
+    elapsed, (tot_in,), reduced, verified = reduce_over_ranks(dist if world > 1 else None, dev, elapsed, local,
+                                                              [st["bytes_in"]])
+    tot_in = int(tot_in)
     names = list(eng.type_names)
     if rank != 0:
         return None

@@ -181,4 +181,7 @@ def test_config5_long_rows(c5, c5_comp, c5_oracle):
     for i, t in enumerate(texts):
         red, fs = O.redact(t, c5_oracle, None)
         assert res.text(i) == red, i
+        m = res.spans["utt"] == i             # spans too, not only the redacted bytes
+        got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"])) for s in res.spans[m]]
+        assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], i
     eng.close()

@@ -74,3 +74,63 @@ def test_shard_of_is_stable_and_balanced():
         counts = np.bincount([D.shard_of(c, world) for c in ids], minlength=world)
         assert counts.min() > 0.8 * len(ids) / world
         assert [D.shard_of(c, world) for c in ids[:50]] == [D.shard_of(c, world) for c in ids[:50]]
+
+
+# ---------------------------------------------------------------- string conversation ids, service level
+def _svc_worker(rank, world, port, payloads, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from test_service import Clock, OracleEngine
+    from oracle import pii_oracle as O
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D, S = pkg("distributed"), pkg("service")
+    cfg = O.RuleConfig.load()
+    mine = [p for p in payloads if D.shard_of(p["conversation_id"], world) == rank]
+    svc = S.PiiService(engine=OracleEngine(cfg, n_slots=8), clock=Clock(), time_base="payload")
+    res = svc.process_pubsub_batch(mine)
+    h = np.zeros(len(cfg.type_names) + 1, dtype=np.int64)
+    for r in res:
+        red, fs = O.redact(r["original_text"].encode(), cfg, None)
+        h[-1] += 1
+    out[rank] = (res, D.reduce_histogram(h).tolist())
+    dist.destroy_process_group()
+
+
+def test_string_conversation_ids_shard_and_match_one_process():
+    """Config 4's sharding with the reference's string conversation ids (UUID-like, e2e_test.py): every
+    rank serves the conversations shard_of() gives it with its own service and context table; the
+    union of the ranks' redacted payloads equals one process serving everything, and the all_reduce
+    sees every row exactly once."""
+    import json
+    import random
+    from oracle import pii_oracle as O
+    S = pkg("service")
+    tr = json.load(open(os.path.join(ROOT, "tests", "golden", "transcripts.json")))
+    pay = []
+    for k in range(6):
+        for name, t in tr.items():
+            cid = f"conv-{k:02d}-{t['conversation_id']}"
+            for e in t["entries"]:
+                pay.append({"conversation_id": cid, "original_entry_index": e["i"], "participant_role": e["role"],
+                            "text": e["text"], "user_id": "u", "start_timestamp_usec": e["ts"]})
+    random.Random(3).shuffle(pay)
+    D = pkg("distributed")
+    assert {D.shard_of(p["conversation_id"], 2) for p in pay} == {0, 1}
+    mgr = tmp.Manager()
+    out = mgr.dict()
+    tmp.spawn(_svc_worker, args=(2, _free_port(), pay, out), nprocs=2, join=True)
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_service import Clock, OracleEngine
+    one = S.PiiService(engine=OracleEngine(O.RuleConfig.load(), n_slots=8), clock=Clock(), time_base="payload")
+    want = {(r["conversation_id"], r["original_entry_index"]): r for r in one.process_pubsub_batch(pay)}
+    got = {}
+    for rank in range(2):
+        res, h = out[rank]
+        assert h[-1] == len(pay)
+        for r in res:
+            got[(r["conversation_id"], r["original_entry_index"])] = r
+    assert got == want

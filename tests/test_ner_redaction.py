@@ -314,3 +314,11 @@ def test_device_ner_on_the_redaction_path(eng, oracle_cfg, ner_model):
     for i in clean:
         assert out[int(oo[i]):int(oo[i + 1])] == exp_hf[i][0], i
     assert len(clean) > 0
+    # rows on which the bf16 detector labels every token as the fp32 model does redact exactly as
+    # oracle + HF; with seeded random weights many tokens sit near a tie (only 10 of 320 rows clear the
+    # 0.1 margin on every token), so the bar is that most rows agree token for token (not
+    # just "> 0 rows")
+    agree = [i for i in range(n) if (gpu_lab[i][real[i]] == hf_lab[i][real[i]]).all()]
+    for i in agree:
+        assert out[int(oo[i]):int(oo[i + 1])] == exp_hf[i][0], i
+    assert len(agree) >= 0.75 * n, (len(agree), n)
