@@ -36,7 +36,6 @@ using namespace pii;
 
 namespace {
 
-constexpr int P_MAX = 64;          // detector patterns handled by k_select's private state
 constexpr int NE_MAX = 2;          // excluder patterns
 constexpr int SCAN_BLOCK = 768;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
 constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
@@ -2956,12 +2955,13 @@ constexpr int WIN_TILE = 64;       // windows per k_win_redact workgroup
 constexpr int WHOT_BITS = 16;      // hotword rules whose proximity results are kept resident
 struct WCand {          // one resident candidate (16 B)
     uint32_t s, e;      // match [s, e), relative to its utterance
-    uint8_t p;          // detector pattern
+    uint16_t p;         // detector pattern (any rule set: config 5 has 544)
     uint8_t need;       // predecessors its longest before-window needs (0: it stays inside the utterance)
+    uint8_t pad;
     uint16_t hot;       // bit h: hotword rule h hits, proximity windows clipped to the utterance
     uint16_t hotx;      // bit h: ... before-window over the (up to `need`) preceding utterances
-    uint16_t pad;
 };
+static_assert(sizeof(WCand) == 16, "WCand is one 16-byte record in the ring arena");
 struct WDesc {          // one resident utterance of a conversation's history ring (16 B)
     uint32_t off;       // arena offset (16-aligned): nc WCands, then the text bytes
     uint32_t len;
@@ -3071,6 +3071,7 @@ __device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WinRing& W
 
 // per matched pair: validator + every hotword rule the pattern's type has in ANY context variant,
 // proximity windows clipped to the utterance -> PairRes.lik = 0 valid / -1 invalid, phot = rule bits
+template <bool GI>
 __global__ __launch_bounds__(PAIR_BLOCK) void k_win_eval(const uint4* __restrict__ img, const LdsImage li,
                                                          const uint8_t* __restrict__ text0,
                                                          const uint64_t* __restrict__ offs,
@@ -3081,7 +3082,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_win_eval(const uint4* __restrict
                                                          const int32_t* __restrict__ pend,
                                                          PairRes* __restrict__ pres, uint32_t* __restrict__ phot) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
     const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
@@ -3140,7 +3141,7 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
                                                    const uint32_t* __restrict__ lane_np,
                                                    const EvLoc* __restrict__ evloc, const PairRes* __restrict__ pres,
                                                    const int32_t* __restrict__ pend, const uint32_t* __restrict__ phot,
-                                                   uint64_t pair_cap, int n_pat, WCand* __restrict__ wc,
+                                                   uint64_t pair_cap, uint2* __restrict__ spill, WCand* __restrict__ wc,
                                                    uint32_t* __restrict__ wc_first, uint32_t* __restrict__ wc_n,
                                                    const uint32_t* __restrict__ err) {
     if (*err & ERR_ABORT) return;
@@ -3151,7 +3152,10 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
     if (np == 0 || base + np > pair_cap) return;
     uint32_t u = 0xffffffffu, k = 0, uf = 0;
     int lp[LIVE], le[LIVE];
-    uint32_t cur_s[P_MAX];
+    // more than LIVE patterns live in one row: their (pattern, end) list in the lane's pair-queue slots
+    // of `spill` (k_select's buffer, unused on the window path), as in select_run
+    uint2* __restrict__ sp = spill + base;
+    uint32_t n_spill = 0;
     bool spilled = false;
 #pragma unroll
     for (int q = 0; q < LIVE; ++q) {
@@ -3179,7 +3183,8 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         const int p = P.p;
         int prev_end = -1;
         if (spilled) {
-            prev_end = (int)cur_s[p];
+            for (uint32_t q = 0; q < n_spill; ++q)
+                if ((int)sp[q].x == p) prev_end = (int)sp[q].y;
         } else {
 #pragma unroll
             for (int q = 0; q < LIVE; ++q)
@@ -3187,7 +3192,10 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         }
         if (s < prev_end) return;                    // inside p's previous match (finditer)
         if (spilled) {
-            cur_s[p] = (uint32_t)e;
+            uint32_t q = 0;
+            while (q < n_spill && (int)sp[q].x != p) ++q;
+            sp[q] = make_uint2((uint32_t)p, (uint32_t)e);
+            if (q == n_spill) ++n_spill;
         } else {
             int slot = -1;
 #pragma unroll
@@ -3206,11 +3214,11 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
                         le[q] = e;
                     }
             } else {
-                for (int q = 0; q < n_pat; ++q) cur_s[q] = 0;
+                n_spill = 0;
 #pragma unroll
                 for (int q = 0; q < LIVE; ++q)
-                    if (lp[q] >= 0) cur_s[lp[q]] = (uint32_t)le[q];
-                cur_s[p] = (uint32_t)e;
+                    if (lp[q] >= 0) sp[n_spill++] = make_uint2((uint32_t)lp[q], (uint32_t)le[q]);
+                sp[n_spill++] = make_uint2((uint32_t)p, (uint32_t)e);
                 spilled = true;
             }
         }
@@ -3218,11 +3226,11 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         WCand C;
         C.s = (uint32_t)s;
         C.e = (uint32_t)e;
-        C.p = (uint8_t)p;
+        C.p = (uint16_t)p;
         C.need = 0;
+        C.pad = 0;
         C.hot = (uint16_t)phot[base + i];
         C.hotx = C.hot;
-        C.pad = 0;
         wc[base + k++] = C;
     };
     // the lane's pend[] run in prefetched 16-entry groups, matched pairs only (as in k_select)
@@ -3258,12 +3266,13 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
 // utterances are evaluated ONCE, here, over the predecessors the row's own window holds (those are
 // the only ones any later window can hold before it): hotx + need.  A later window in which the
 // utterance has j >= need predecessors reuses hotx; j == 0 (window start) reuses hot.
+template <bool GI>
 __global__ __launch_bounds__(256) void k_win_halo(const uint4* __restrict__ img, const LdsImage li, const WinRing W,
                                                   const WinBatch B, WCand* __restrict__ wc,
                                                   const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & (ERR_ABORT | ERR_SLOT)) return;
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[EV_TRANS]), lb + li.off[EV_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[EV_HDESC]);
     const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
@@ -3329,6 +3338,7 @@ __global__ __launch_bounds__(256) void k_win_plan(const WinRing W, const WinBatc
 // per window: the window's context variant -> hotword likelihoods (resident bits, or a re-run over
 // the halo when a proximity window crosses a '\n'), min likelihood, exclusion, overlap; findings in
 // window coordinates, output length
+template <bool GI>
 __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                     const WinRing W, const WinBatch B,
                                                     const int16_t* __restrict__ win_ctx,
@@ -3337,7 +3347,7 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
                                                     uint32_t* __restrict__ wout_len, uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & (ERR_ABORT | ERR_SLOT)) return;
-    const uint8_t* lb = load_image(img, li.total, lds4);
+    const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[WS_TRANS]), lb + li.off[WS_CMAP]};
     const int32_t* hdesc = reinterpret_cast<const int32_t*>(lb + li.off[WS_HDESC]);
     const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[WS_HRULE]);
@@ -3862,7 +3872,6 @@ struct pii_engine {
     AccTabs acct{};
     uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs<.., MULTI>)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
-    bool wsel_ok = true;               // the window re-scan's images fit in LDS
     int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
@@ -4619,11 +4628,11 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
                            st)))
         return rc;
     if (n_utt > 0 && n_chunks > 0) {
-        k_win_eval<<<e->n_seg, PAIR_BLOCK, e->img_eval.li.total, st>>>(
+        (e->img_eval.global ? k_win_eval<true> : k_win_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(), st>>>(
             e->img_eval.d, e->img_eval.li, text, offs, pcount, e->pair_cap, e->matched, e->mcount, e->n_seg,
             e->evloc, e->pend, e->pres, e->phot);
         k_win_cands<<<(n_chunks + 255) / 256, 256, 0, st>>>(n_chunks, e->lane_pair, e->lane_np, e->evloc, e->pres,
-                                                            e->pend, e->phot, e->pair_cap, R.P, e->wc, e->wc_first,
+                                                            e->pend, e->phot, e->pair_cap, e->spill, e->wc, e->wc_first,
                                                             e->wc_n, e->d_err);
         HIPCHK(hipGetLastError());
     }
@@ -4631,12 +4640,14 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     const WinBatch B{text, offs, slot, e->wc, e->wc_first, e->wc_n, n_utt};
     const uint32_t nb = (n_utt + 255) / 256;
     if (n_utt > 0 && n_chunks > 0)
-        k_win_halo<<<nb, 256, e->img_eval.li.total, st>>>(e->img_eval.d, e->img_eval.li, W, B, e->wc, e->d_err);
+        (e->img_eval.global ? k_win_halo<true> : k_win_halo<false>)<<<nb, 256, e->img_eval.lds(), st>>>(
+            e->img_eval.d, e->img_eval.li, W, B, e->wc, e->d_err);
     HIPCHK(hipEventRecord(e->tev[3], st));
     if (n_utt > 0) {
         k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
         if ((rc = exclusive_scan(e, e->wbound, n_utt, e->wfbase, st))) return rc;
-        k_win_select<<<nb, 256, e->img_wsel.li.total, st>>>(R, e->img_wsel.d, e->img_wsel.li, W, B, wctx, e->wfbase,
+        (e->img_wsel.global ? k_win_select<true> : k_win_select<false>)<<<nb, 256, e->img_wsel.lds(), st>>>(
+            R, e->img_wsel.d, e->img_wsel.li, W, B, wctx, e->wfbase,
                                                              e->wfd_cap, e->wfd, e->n_wfind, e->wout_len, e->d_err);
         HIPCHK(hipGetLastError());
     }
@@ -5060,14 +5071,13 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
             return fail("rule table upload failed");
-        // the window re-scan keeps its tables in LDS (rule sets whose images do not fit cannot enable it)
-        e->wsel_ok = !e->img_wsel.global && !e->img_eval.global;
+        // (the window re-scan's kernels read an image past LDS in place, like the pair kernels)
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first<false>, &e->img_first}, {(const void*)k_pair_eval<false>, &e->img_eval},
             {(const void*)k_select<false, false>, &e->img_sel}, {(const void*)k_sel_fix<false, false>, &e->img_sel},
             {(const void*)k_select<false, true>, &e->img_sel}, {(const void*)k_sel_fix<false, true>, &e->img_sel},
-            {(const void*)k_win_eval, &e->img_eval},
-            {(const void*)k_win_select, &e->img_wsel}, {(const void*)k_win_halo, &e->img_eval}};
+            {(const void*)k_win_eval<false>, &e->img_eval},
+            {(const void*)k_win_select<false>, &e->img_wsel}, {(const void*)k_win_halo<false>, &e->img_eval}};
         for (auto& kb : big)
             if (!kb.second->global && kb.second->li.total > 64 * 1024 &&
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
@@ -5551,10 +5561,12 @@ int pii_window_enable_ex(pii_engine* e, uint32_t window_n, uint32_t slot_bytes, 
     e->wr_cnt = w.cnt;
     e->wr_head = w.head;
     e->wr_arena = w.arena;
-    // the incremental path needs: no detector that consumes '\n' or tests a text edge (a match inside a
-    // window is then its utterance's own match), at most P_MAX patterns, one SCAN group, LDS-resident
-    // tables; any other rule set re-scans the joined windows in full
-    e->win_full = (flags & PII_WINDOW_FULL) || !e->window_ok || e->R.P > P_MAX || e->n_sg > 1 || !e->wsel_ok;
+    // the incremental path needs no detector that consumes '\n' or tests a text edge (a match inside a
+    // window is then its utterance's own match); it takes any number of patterns and SCAN groups
+    // (config 5: the groups' merged pair queue, candidate lists past LIVE patterns spilled like
+    // k_select's) and tables past LDS (read in place); any other rule set re-scans the joined windows
+    // in full
+    e->win_full = (flags & PII_WINDOW_FULL) || !e->window_ok;
     e->win_n = window_n;
     e->win_slot_bytes = slot_bytes;
     return PII_OK;

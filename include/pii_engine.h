@@ -206,10 +206,10 @@ int pii_last_stats(struct pii_engine* e, uint64_t* out, uint32_t n);
  * proximity window crosses a "\n", the context variant, and the output copy.  Output per row =
  * redact("\n".join(window ending at that row), current expected_pii_type) bit-exactly (SURVEY A.9,
  * oracle/pii_oracle.py window_rescan), for every rule set: when no detector can match '\n' or a text
- * edge and the rules fit one LDS-resident SCAN group (the shipped rules), incrementally; otherwise
- * (config-5 scale rule sets, a '\n'-consuming detector) by a FULL re-scan -- the ring then keeps the
- * raw text, every row's "\n"-joined window is materialised in HBM and run through the scan+redact
- * pipeline (one host wait per call for the joined size). */
+ * edge, incrementally (the shipped rules and config-5 scale rule sets alike: any number of patterns
+ * and SCAN groups, tables in LDS or read in place); otherwise (a '\n'-consuming detector) by a FULL
+ * re-scan -- the ring then keeps the raw text, every row's "\n"-joined window is materialised in HBM
+ * and run through the scan+redact pipeline (one host wait per call for the joined size). */
 #define PII_WINDOW_MAX 8
 #define PII_WINDOW_FULL 1   /* pii_window_enable_ex flag / pii_window_mode result: full re-scan */
 /* allocate the per-slot window history (n_conv_slots * slot_bytes of HBM); window_n <= PII_WINDOW_MAX,
