@@ -439,6 +439,8 @@ def main():
     ap.add_argument("--batch-wait-ms", type=float, default=0.5, help="(service) MicroBatcher max_wait")
     ap.add_argument("--window-n", type=int, default=5)
     ap.add_argument("--window-full", action="store_true", help="(window) force the full re-scan of the joined windows")
+    ap.add_argument("--window-rules", choices=["shipped", "config5"], default="shipped",
+                    help="(window) the shipped rules, or config 5's 542-type rule set (7 SCAN groups)")
     ap.add_argument("--stream-gb", type=float, default=100.0, help="(config 4) stream size per node, GB")
     ap.add_argument("--stream-weak", action="store_true", help="(config 4) --stream-gb per GPU instead of per node")
     ap.add_argument("--shard-gb", type=float, default=1.0, help="(config 4) host shard each rank replays, GB")
@@ -1087,9 +1089,17 @@ def window_main(args):
     import torch
     eng_mod = importlib.import_module("context-based-pii_amd.engine")
     C, U, N = args.conversations, args.utt_per_conv, args.window_n
-    bank = synth.build_bank(16384, 16384, seed=synth.SEED)
+    c5path = None
+    if args.window_rules == "config5":          # the re-scan under config 5's 542-type rule set
+        import tempfile
+        c5 = importlib.import_module("context-based-pii_amd.rulegen").Config5()
+        c5path = os.path.join(tempfile.gettempdir(), f"config5_w_{os.getpid()}.json")
+        c5.save(c5path)
+        bank = c5.build_bank()
+    else:
+        bank = synth.build_bank(16384, 16384, seed=synth.SEED)
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and c5path is None:
         cpu = cpu_window_baseline(bank, N, args.cpu_seconds)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
@@ -1105,9 +1115,11 @@ def window_main(args):
     d_oo = torch.empty(C + 1, dtype=torch.int64, device=dev)
     d_sp = torch.empty(span_cap * 16, dtype=torch.uint8, device=dev)
     d_ctx = torch.empty(C, dtype=torch.int16, device=dev)
-    comp = compiler.compile_default()
+    comp = compiler.compile_rules(compiler.Rules.load(c5path)) if c5path else compiler.compile_default()
+    if c5path:
+        os.unlink(c5path)
     eng = eng_mod.Engine(comp.blob, device=0, n_conv_slots=C)
-    eng.window_enable(N, 8192, full=args.window_full)
+    eng.window_enable(N, 8192 if c5path is None else 16384, full=args.window_full)
     torch.cuda.synchronize()
 
     def step(k):
@@ -1162,7 +1174,9 @@ def window_main(args):
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"config3: {C} concurrent conversations, window N={N}, one new utterance per "
                                f"conversation per step (pii_rescan_window_device, {eng.window_mode()} mode), "
-                               f"expected_pii_type context",
+                               f"expected_pii_type context" + (", config-5 rules (542 types, 7 SCAN groups)"
+                                                               if c5path else ""),
+                   "rules": args.window_rules, "mode": eng.window_mode(),
                    "rows_per_step": C, "parallelism": "conversation-sharded x1",
                    "bytes_per_gpu": int(meta.offsets[-1])},
         "windows_per_s": round(K * C / elapsed, 1),

@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
                                                      uint32_t* __restrict__ first_utt, uint32_t* __restrict__ out_len,
                                                      int32_t* __restrict__ kw, uint32_t* __restrict__ wc_n,
                                                      uint32_t* __restrict__ long_rows, uint32_t* __restrict__ long_count,
-                                                     uint64_t decl_base, uint64_t decl_bytes, uint32_t* __restrict__ err) {
+                                                     uint32_t long_cap, uint64_t decl_base, uint64_t decl_bytes,
+                                                     uint32_t* __restrict__ err) {
     const uint32_t u0 = (blockIdx.x * blockDim.x + threadIdx.x) * CI_ROWS;
     if (u0 > n_utt) return;
     const uint64_t base = offs[0];
@@ -224,8 +225,11 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
             // a row that some slice boundary cuts (same test as g_cut)
             if (long_min != NO_CUTS && len > long_min) {
                 const uint64_t kk = ((o[k + 1] - base + r0) >> lane_shift) + 1;      // first boundary after its start
-                if (kk < n_chunks && ((int64_t)(kk << lane_shift) - (int64_t)r0) < (int64_t)(o[k + 2] - base))
-                    long_rows[atomicAdd(long_count, 1u)] = u;
+                if (kk < n_chunks && ((int64_t)(kk << lane_shift) - (int64_t)r0) < (int64_t)(o[k + 2] - base)) {
+                    const uint32_t at = atomicAdd(long_count, 1u);
+                    if (at < long_cap) long_rows[at] = u;
+                    else atomicOr(err, (uint32_t)ERR_STITCH);      // (sized by ensure_scratch: internal)
+                }
             }
         }
     }
@@ -745,7 +749,7 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g,
     uint32_t& s_np = s_prev[FIX_Q + 1];
     uint32_t& s_full = s_prev[FIX_Q + 2];
     const uint32_t nrows = *long_count;
-    if (blockIdx.x >= nrows || (*err & ERR_ARGS)) return;
+    if (blockIdx.x >= nrows || (*err & (ERR_ARGS | ERR_STITCH))) return;     // (STITCH: the row list overflowed)
     {
         const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
@@ -2248,7 +2252,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint
                                                         uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     __shared__ uint32_t sh[ROW_BLOCK / 64];
     __shared__ uint32_t s_carry;
-    if (*err & ERR_ABORT) return;
+    if (*err & (ERR_ABORT | ERR_STITCH)) return;
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         uint32_t ca, kb;
         int64_t s_r, e_r;
@@ -2281,7 +2285,7 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
                                                  const uint32_t* __restrict__ long_count,
                                                  const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & ERR_ABORT) return;
+    if (*err & (ERR_ABORT | ERR_STITCH)) return;
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
@@ -2305,7 +2309,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_rowlen(const Geo g, const uint32_
                                                      uint32_t* __restrict__ out_len, const uint32_t* __restrict__ err) {
     __shared__ int32_t sh[ROW_BLOCK / 64];
     __shared__ int32_t s_carry;
-    if (*err & ERR_ABORT) return;
+    if (*err & (ERR_ABORT | ERR_STITCH)) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         const uint32_t r = long_rows[ri];
@@ -4108,7 +4112,11 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         e->cap_lanes = nl;
         e->cap_bsum = 0;
     }
-    const uint64_t need_long = std::min<uint64_t>((uint64_t)n_utt + 1, bytes / 1024 + 2);
+    // rows cut into lanes (k_chunk_index's long-row list): a long row is longer than long_min = 2 lanes,
+    // and lanes shrink to 2^MIN_LANE_SHIFT bytes for small batches -- so at most bytes / 256 of them
+    // (sizing this for 1 KiB lanes overflowed the list on a full window re-scan of 50k conversations,
+    // whose ~600-byte joined windows are all long rows of 256-byte lanes)
+    const uint64_t need_long = std::min<uint64_t>((uint64_t)n_utt + 1, bytes / (2u << MIN_LANE_SHIFT) + 2);
     if (need_long > e->cap_long) {
         if ((rc = grow(e, e->long_rows, need_long))) return rc;
         e->cap_long = need_long;
@@ -4261,7 +4269,8 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         k_chunk_index<<<(n_utt / CI_ROWS + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
                                                                 e->long_min, R.kw_always_min, e->first_utt,
                                                                 e->out_len, e->kw, win_ctx ? e->wc_n : nullptr,
-                                                                e->long_rows, e->long_count, base, total_bytes, e->d_err);
+                                                                e->long_rows, e->long_count, (uint32_t)e->cap_long, base,
+                                                                total_bytes, e->d_err);
         if (n_chunks > 0) {
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
