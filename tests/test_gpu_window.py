@@ -238,3 +238,24 @@ def test_window_tables_outside_the_scratch_limit_and_resize(compiled, oracle_cfg
             eng.context_resize(20)                                  # shrinking is refused
     finally:
         eng.close()
+
+
+def test_full_window_many_long_joined_rows(compiled, oracle_cfg):
+    """Regression (r04): in a full re-scan the joined windows of thousands of conversations are all
+    long rows of small (128-256 B) lanes; the long-row list was sized for 1 KiB lanes and overflowed
+    (illegal access at 50k conversations).  A fresh engine, 2000 conversations x 6 steps vs the oracle."""
+    from oracle import pii_oracle as O
+    E, synth = pkg("engine"), pkg("synth")
+    eng = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
+    try:
+        eng.window_enable(5, 8192, full=True)
+        bank = synth.build_bank(400, 900, seed=61)
+        corp = synth.make_corpus(2000, 6, bank, seed=62)
+        per_conv = {}
+        for r in _stream(corp, 1):
+            per_conv.setdefault(r[0], []).append(r)
+        state = None
+        for k in range(6):
+            state = _check(eng, oracle_cfg, [[per_conv[c][k] for c in sorted(per_conv)]], state=state)
+    finally:
+        eng.close()
