@@ -26,6 +26,7 @@ import hashlib
 import io
 import json
 import os
+import dataclasses
 import re
 import struct
 import sys
@@ -409,7 +410,7 @@ def relax_items(items, budget: int):
     the exact FIRST DFA confirms each).  Bounded repeats are widened ({lo,hi} -> {min(lo,k)} X*),
     the sequence is cut after `budget` consuming characters, an alternation ends the prefix."""
     out = []
-    for op, av in items:
+    for i, (op, av) in enumerate(items):
         if op == C.AT:
             out.append((op, av))
             continue
@@ -449,6 +450,15 @@ def relax_items(items, budget: int):
                         return out, False, 0
                 if hi != lo:
                     return out, False, 0
+                continue
+            if hi != lo and hi != C.MAXREPEAT and hi <= budget and all(o == C.AT for o, _ in items[i + 1:]):
+                # a bounded repeat that ends the sequence and fits whole is kept exact, so the trailing
+                # assertion still filters -- \b\d{3,4}\b no longer fires at every longer digit run
+                # (inside a sequence, widening spends only `lo` of the budget on it: more of what
+                # follows is kept, e.g. IP_ADDRESS's dots)
+                out.extend(sub * lo)
+                out.append((C.MAX_REPEAT, (0, hi - lo, sub)))
+                budget -= hi
                 continue
             n = min(lo, budget)
             out.extend(sub * n)
@@ -873,6 +883,7 @@ SCAN_GROUP_BYTES = 62 * 1024    # D table of a scan group >= 1 that keeps 16-bit
                                 # k_scan workgroups per CU); its K is a 1-row never-accepting stub
 SCAN_WIDE_BYTES = 124 * 1024    # a WIDE group >= 1 (engine: rows padded to 4 entries, entries = offset / 2,
                                 # one workgroup per CU): up to 64k transitions
+SPILL_PREFIX = 10               # prefix of the built-ins moved out of group 0 (plan_scan_groups)
 SCAN_GROUPS_MAX = 8             # k_pairs merges at most this many per-group event lists per lane
 DICT_SCAN_PREFIX = 4            # SCAN prefix of dictionary infoTypes (Rules)
 
@@ -933,7 +944,20 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
                         "info_types", [])}
     base = [p for p in rules.patterns if not p.custom or p.type_name in excl]
     rest = sorted((p for p in rules.patterns if p.custom and p.type_name not in excl), key=_prefix_key)
-    g0 = _scan_dfa_fit(base, budget, limit0)
+    # group 0 keeps the declared prefixes: when they do not fit beside K (config 5's larger keyword
+    # automaton), the non-excluder built-ins with the longest declared prefixes move to a group of their
+    # own (one more k_scan pass) rather than every built-in falling back to `budget` characters --
+    # short digit-run prefixes fire at every digit run of the custom types' ids
+    spill: List[Pattern] = []
+    g0 = _scan_dfa(base, budget, limit0)
+    if g0 is None:
+        spill = [p for p in base if p.type_name not in excl and p.scan_prefix]
+        base = [p for p in base if not (p.type_name not in excl and p.scan_prefix)]
+        g0 = _scan_dfa(base, budget, limit0) if base else None
+    if g0 is None:
+        spill, base = [], spill + base
+        base.sort(key=lambda p: p.pid)
+        g0 = _scan_dfa_fit(base, budget, limit0)
     if g0 is None:
         raise RuleError("the built-in detectors' SCAN automaton does not fit k_scan's LDS")
     out = [(base, g0)]
@@ -963,6 +987,15 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
         h = len(pats) // 2
         split(pats[:h])
         split(pats[h:])
+    if spill:
+        # the spilled built-ins have a table of their own: their prefixes may grow to SPILL_PREFIX
+        # (digit-run detectors: a 7-digit prefix still fires at every 7-9 digit custom id)
+        long = [dataclasses.replace(p, scan_prefix=max(p.scan_prefix, SPILL_PREFIX)) for p in spill]
+        m = _scan_dfa(long, budget, SCAN_GROUP_BYTES)
+        if m is not None:
+            out.append((sorted(long, key=lambda p: p.pid), m))
+        else:
+            split(sorted(spill, key=lambda p: p.pid))
     if rest:
         split(rest)
     if len(out) > SCAN_GROUPS_MAX:
