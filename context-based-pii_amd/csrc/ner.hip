@@ -33,6 +33,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {      // round to nearest eve
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int32_t CLS_ID = 101, SEP_ID = 102, PAD_ID = 0;     // (ner.py CLS, SEP, PAD)
 constexpr int G_THREADS = 256;
+#ifndef GEMM_PIPE
+#define GEMM_PIPE 1         // k_gemm2 (double-buffered slabs); 0 = the single-buffer k_gemm
+#endif
+#ifndef GEMM_BIG
+#define GEMM_BIG 1          // allow the 256-row k_gemm2 tiles
+#endif
 
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2 };
 
@@ -160,6 +166,145 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
         }
         __syncthreads();
     }
+    (void)M;
+}
+
+// Epilogue of one 64-row group: the accumulators of the two wavefronts owning rows [64 g, 64 g + 64) go
+// through LDS as a row-major f32 [64][128] image (C/D map of 32x32x16: col = lane & 31, row = (reg & 3)
+// + 8 (reg >> 2) + 4 (lane >> 5)); every thread then finishes 8-column chunks (bias, GELU / residual)
+// with 16-byte loads of the residual and 16-byte stores of C.
+template <int EPI, int NT>
+__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float* sC, int mine, int wn, const float* bias,
+                                              const uint16_t* R, uint16_t* C, int grow0, int n0, int N) {
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    if (mine) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int row = 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    sC[row * GB_N + wn + 32 * j + r] = acc[i][j][reg];
+                }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 1024 / NT; ++t) {
+        const int q = tid + t * NT, row = q >> 4, c8 = (q & 15) * 8;
+        const float4 x0 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8);
+        const float4 x1 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8 + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const int grow = grow0 + row, gcol = n0 + c8;
+        if (bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+            const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        if (EPI == EPI_GELU) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+        } else if (EPI == EPI_RESID) {
+            const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)grow * N + gcol);
+            const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[2 * e] += bf2f((uint16_t)(rw[e] & 0xffffu));
+                v[2 * e + 1] += bf2f((uint16_t)(rw[e] >> 16));
+            }
+        }
+        uint4 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = o;
+    }
+    __syncthreads();
+}
+
+// The pipelined form: BM x 128 output tiles (BM = 256: 8 wavefronts, BM = 128: 4), each wavefront a
+// 64 x 64 block as 2 x 2 v_mfma_f32_32x32x16_bf16, and TWO LDS slab buffers -- the DMA of K-slab k+1
+// (global_load_lds, 16 B per lane, source-swizzled as k_gemm) is issued before the MFMAs of slab k, so
+// it runs under them, and one barrier per slab both retires it and frees slab k's buffer for slab k+2.
+// BM = 256 for the N >= 2304 projections (>= 576 tiles, one 96 KiB workgroup per CU), BM = 128 for
+// N = 768 (384 tiles, 64 KiB, two per CU).  All LDS is one __shared__ array (a second one would make
+// hipcc drain the DMA queue before every first ds_read, cdna_hip_programming.md §5 item 4(a)).
+template <int EPI, int BM>
+__global__ __launch_bounds__(BM * 2) void k_gemm2(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
+                                                  const float* __restrict__ bias, const uint16_t* __restrict__ R,
+                                                  uint16_t* __restrict__ C, int M, int N, int K) {
+    constexpr int NW = BM / 32, NT = NW * 64;
+    constexpr int SA = BM * GB_K, SB = GB_N * GB_K;           // slab elements
+    constexpr int IA = (SA * 2 / 1024) / NW, IB = (SB * 2 / 1024) / NW;   // 1 KiB DMA instructions per wave
+    static_assert(IA * NW * 512 == SA && IB * NW * 512 == SB, "slabs are whole 1 KiB DMA instructions per wave");
+    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (SA + SB)];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tiles_n = N / GB_N;
+    const int nwg = (int)gridDim.x, orig = (int)blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int tm = bid / tiles_n, tn = bid % tiles_n;
+    const int m0 = tm * BM, n0 = tn * GB_N;
+    const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+    const uint16_t* srcA[IA];
+    const uint16_t* srcB[IB];
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+        const int q = (i * NW + wave) * 64 + lane, row = q >> 3, pos = q & 7;
+        srcA[i] = A + (size_t)(m0 + row) * K + 8 * (pos ^ (row & 7));
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+        const int q = (i * NW + wave) * 64 + lane, row = q >> 3, pos = q & 7;
+        srcB[i] = W + (size_t)(n0 + row) * K + 8 * (pos ^ (row & 7));
+    }
+    auto stage = [&](int k0, int buf) {
+        uint16_t* sA = smem + buf * (SA + SB);
+        uint16_t* sB = sA + SA;
+#pragma unroll
+        for (int i = 0; i < IA; ++i)
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcA[i] + k0), (lptr_t)(sA + (i * NW + wave) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < IB; ++i)
+            __builtin_amdgcn_global_load_lds((gptr_t)(srcB[i] + k0), (lptr_t)(sB + (i * NW + wave) * 512), 16, 0, 0);
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    const int r = lane & 31, h = lane >> 5;
+    const int nk = K / GB_K;
+    stage(0, 0);
+    __syncthreads();                               // (its fence waits for the DMA: slab 0 is in LDS)
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) stage((kt + 1) * GB_K, buf ^ 1);      // runs under this slab's MFMAs
+        const uint16_t* sA = smem + buf * (SA + SB);
+        const uint16_t* sB = sA + SA;
+#pragma unroll
+        for (int ks = 0; ks < GB_K / 16; ++ks) {
+            bf16x8 fa[2], fb[2];
+            const int c = 2 * ks + h;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ra = wm + 32 * i + r, rb = wn + 32 * i + r;
+                fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
+                fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();                           // slab k+1 landed (DMA retired); slab k's buffer is free
+    }
+    float* sC = reinterpret_cast<float*>(smem);    // 32 KiB f32 image per 64-row group
+#pragma unroll
+    for (int g = 0; g < BM / 64; ++g)
+        gemm_epilogue<EPI, NT>(acc, sC, wm == 64 * g, wn, bias, R, C, m0 + 64 * g, n0, N);
     (void)M;
 }
 
@@ -550,11 +695,28 @@ int ner_gemm(const void* A, const void* W, const void* bias, const void* resid, 
              int epi, void* stream) {
     if (!A || !W || !C || M % GB_M || N % GB_N || K % GB_K || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !resid))
         return -1;
+    const uint16_t *a = static_cast<const uint16_t*>(A), *w = static_cast<const uint16_t*>(W);
+    const uint16_t* rs = static_cast<const uint16_t*>(resid);
+    uint16_t* c = static_cast<uint16_t*>(C);
+    const float* b = static_cast<const float*>(bias);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (GEMM_PIPE) {
+        // 256-row tiles when they still give every CU at least two tiles, else 128-row tiles
+        const bool big = GEMM_BIG && M % 256 == 0 && (M / 256) * (N / GB_N) >= 512;
+        if (big) {
+            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 256> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 256>
+                                                                                     : k_gemm2<EPI_BIAS, 256>;
+            kern<<<(M / 256) * (N / GB_N), 512, 0, st>>>(a, w, b, rs, c, M, N, K);
+        } else {
+            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 128> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 128>
+                                                                                     : k_gemm2<EPI_BIAS, 128>;
+            kern<<<(M / 128) * (N / GB_N), 256, 0, st>>>(a, w, b, rs, c, M, N, K);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     const int blocks = (M / GB_M) * (N / GB_N);
     auto kern = epi == EPI_GELU ? k_gemm<EPI_GELU> : epi == EPI_RESID ? k_gemm<EPI_RESID> : k_gemm<EPI_BIAS>;
-    kern<<<blocks, G_THREADS, 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(W), static_cast<const float*>(bias),
-        static_cast<const uint16_t*>(resid), static_cast<uint16_t*>(C), M, N, K);
+    kern<<<blocks, G_THREADS, 0, st>>>(a, w, b, rs, c, M, N, K);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
