@@ -22,6 +22,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {      // round to nearest even (NaN kept quiet)
@@ -30,14 +31,35 @@ __device__ __forceinline__ uint16_t f2bf(float f) {      // round to nearest eve
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
+// exact (erf) GELU with erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 output
+// rounding): one reciprocal, one exp, five FMAs and no branches -- ocml's erff branches per lane, which
+// made the FFN-up epilogue a sizeable part of that GEMM
+__device__ __forceinline__ float gelu_erf(float v) {
+    const float x = v * 0.70710678118654752f, ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+    const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                             0.254829592f);
+    const float y = 1.f - p * __expf(-ax * ax);
+    return 0.5f * v * (1.f + copysignf(y, x));
+}
+
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int32_t CLS_ID = 101, SEP_ID = 102, PAD_ID = 0;     // (ner.py CLS, SEP, PAD)
 constexpr int G_THREADS = 256;
 #ifndef GEMM_PIPE
 #define GEMM_PIPE 1         // k_gemm2 (double-buffered slabs); 0 = the single-buffer k_gemm
 #endif
+#ifndef GEMM_MF
+#define GEMM_MF 1           // k_gemm2 MFMA shape: 0 = 32x32x16, 1 = 16x16x32
+#endif
+#ifndef GEMM_NB
+#define GEMM_NB 2           // k_gemm2 LDS slab buffers: 2 (one slab in flight) or 3 (two, counted vmcnt)
+#endif
+#ifndef GEMM_PRIO
+#define GEMM_PRIO 1         // raise the wave priority over each MFMA block (s_setprio)
+#endif
 #ifndef GEMM_BIG
-#define GEMM_BIG 1          // allow the 256-row k_gemm2 tiles
+#define GEMM_BIG 0          // allow the 256-row k_gemm2 tiles
 #endif
 
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2 };
@@ -147,7 +169,7 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
             }
             if (EPI == EPI_GELU) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+                for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
             } else if (EPI == EPI_RESID) {
                 const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)grow * N + gcol);
                 const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
@@ -169,28 +191,16 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(const uint16_t* __restrict__
     (void)M;
 }
 
-// Epilogue of one 64-row group: the accumulators of the two wavefronts owning rows [64 g, 64 g + 64) go
-// through LDS as a row-major f32 [64][128] image (C/D map of 32x32x16: col = lane & 31, row = (reg & 3)
-// + 8 (reg >> 2) + 4 (lane >> 5)); every thread then finishes 8-column chunks (bias, GELU / residual)
-// with 16-byte loads of the residual and 16-byte stores of C.
-template <int EPI, int NT>
-__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float* sC, int mine, int wn, const float* bias,
-                                              const uint16_t* R, uint16_t* C, int grow0, int n0, int N) {
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    if (mine) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const int row = 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    sC[row * GB_N + wn + 32 * j + r] = acc[i][j][reg];
-                }
-    }
+// Epilogue of one 64-row group: the accumulators of the two wavefronts owning rows [64 g, 64 g + 64) are
+// written to LDS as a row-major f32 [64][128] image by the caller; every thread then finishes 8-column
+// chunks (bias, GELU / residual) with 16-byte loads of the residual and 16-byte stores of C.
+template <int EPI, int NT, int ROWS>
+__device__ __forceinline__ void gemm_finish(const float* sC, const float* bias, const uint16_t* R, uint16_t* C,
+                                            int grow0, int n0, int N) {
+    const int tid = threadIdx.x;
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 1024 / NT; ++t) {
+    for (int t = 0; t < ROWS * 16 / NT; ++t) {
         const int q = tid + t * NT, row = q >> 4, c8 = (q & 15) * 8;
         const float4 x0 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8);
         const float4 x1 = *reinterpret_cast<const float4*>(sC + row * GB_N + c8 + 4);
@@ -204,7 +214,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float* 
         }
         if (EPI == EPI_GELU) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+            for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
         } else if (EPI == EPI_RESID) {
             const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)grow * N + gcol);
             const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
@@ -231,7 +241,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float* 
 // BM = 256 for the N >= 2304 projections (>= 576 tiles, one 96 KiB workgroup per CU), BM = 128 for
 // N = 768 (384 tiles, 64 KiB, two per CU).  All LDS is one __shared__ array (a second one would make
 // hipcc drain the DMA queue before every first ds_read, cdna_hip_programming.md §5 item 4(a)).
-template <int EPI, int BM>
+template <int EPI, int BM, int MF, int NB>
 __global__ __launch_bounds__(BM * 2) void k_gemm2(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
                                                   const float* __restrict__ bias, const uint16_t* __restrict__ R,
                                                   uint16_t* __restrict__ C, int M, int N, int K) {
@@ -239,7 +249,11 @@ __global__ __launch_bounds__(BM * 2) void k_gemm2(const uint16_t* __restrict__ A
     constexpr int SA = BM * GB_K, SB = GB_N * GB_K;           // slab elements
     constexpr int IA = (SA * 2 / 1024) / NW, IB = (SB * 2 / 1024) / NW;   // 1 KiB DMA instructions per wave
     static_assert(IA * NW * 512 == SA && IB * NW * 512 == SB, "slabs are whole 1 KiB DMA instructions per wave");
-    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (SA + SB)];
+    __shared__ __attribute__((aligned(16))) uint16_t smem[NB * (SA + SB)];
+    // epilogue rows per pass: as many 64-row groups of the f32 [rows][128] image as the slab buffers hold
+    constexpr int EG_FIT = (NB * (SA + SB) * 2) / (GB_N * 4) / 64 * 64;
+    constexpr int EG = BM <= EG_FIT ? BM : BM / 2 <= EG_FIT ? BM / 2 : 64;
+    static_assert(EG >= 64 && BM % EG == 0, "epilogue group");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tiles_n = N / GB_N;
     const int nwg = (int)gridDim.x, orig = (int)blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
@@ -269,42 +283,158 @@ __global__ __launch_bounds__(BM * 2) void k_gemm2(const uint16_t* __restrict__ A
         for (int i = 0; i < IB; ++i)
             __builtin_amdgcn_global_load_lds((gptr_t)(srcB[i] + k0), (lptr_t)(sB + (i * NW + wave) * 512), 16, 0, 0);
     };
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-    const int r = lane & 31, h = lane >> 5;
     const int nk = K / GB_K;
     stage(0, 0);
-    __syncthreads();                               // (its fence waits for the DMA: slab 0 is in LDS)
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) stage((kt + 1) * GB_K, buf ^ 1);      // runs under this slab's MFMAs
-        const uint16_t* sA = smem + buf * (SA + SB);
-        const uint16_t* sB = sA + SA;
+    if (NB == 2) __syncthreads();                  // (its fence waits for the DMA: slab 0 is in LDS)
+    float* sC = reinterpret_cast<float*>(smem);    // f32 [EG][128] epilogue image (after the loop)
+    if (NB == 3) {
+        // three slab buffers, two slabs in flight: slab k+2 is issued right after the barrier that
+        // retires slab k, so the DMA spans a whole slab of MFMAs more; the barrier is a raw s_barrier
+        // after a COUNTED vmcnt (a __syncthreads() fence would drain the DMA queue to 0,
+        // cdna_hip_programming.md "Pipelining across barriers")
+        static_assert(MF == 1, "three-buffer ring: 16x16x32 form only");
+        f32x4 acc[4][4];
 #pragma unroll
-        for (int ks = 0; ks < GB_K / 16; ++ks) {
-            bf16x8 fa[2], fb[2];
-            const int c = 2 * ks + h;
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ra = wm + 32 * i + r, rb = wn + 32 * i + r;
-                fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
-                fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+        const int r = lane & 15, h = lane >> 4;
+        if (nk > 1) stage(GB_K, 1);
+        int buf = 0, nbuf = 2;
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IA + IB) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slab k-1 are done
+            __builtin_amdgcn_s_barrier();
+            if (kt + 2 < nk) stage((kt + 2) * GB_K, nbuf);         // into slab k-1's buffer
+            const uint16_t* sA = smem + buf * (SA + SB);
+            const uint16_t* sB = sA + SA;
+#pragma unroll
+            for (int ks = 0; ks < GB_K / 32; ++ks) {
+                bf16x8 fa[4], fb[4];
+                const int c = 4 * ks + h;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ra = wm + 16 * i + r, rb = wn + 16 * i + r;
+                    fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
+                    fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            buf = buf == 2 ? 0 : buf + 1;
+            nbuf = nbuf == 2 ? 0 : nbuf + 1;
         }
-        __syncthreads();                           // slab k+1 landed (DMA retired); slab k's buffer is free
-    }
-    float* sC = reinterpret_cast<float*>(smem);    // 32 KiB f32 image per 64-row group
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();              // every wave is done with the slabs: sC may overwrite them
 #pragma unroll
-    for (int g = 0; g < BM / 64; ++g)
-        gemm_epilogue<EPI, NT>(acc, sC, wm == 64 * g, wn, bias, R, C, m0 + 64 * g, n0, N);
+        for (int g = 0; g < BM / EG; ++g) {
+            if (wm >= EG * g && wm < EG * (g + 1)) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg)
+                            sC[(wm - EG * g + 16 * i + 4 * h + reg) * GB_N + wn + 16 * j + r] = acc[i][j][reg];
+            }
+            gemm_finish<EPI, NT, EG>(sC, bias, R, C, m0 + EG * g, n0, N);
+        }
+    } else if (MF == 0) {
+        // 2 x 2 v_mfma_f32_32x32x16_bf16 per 16-deep step
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+        const int r = lane & 31, h = lane >> 5;
+        for (int kt = 0; kt < nk; ++kt) {
+            const int buf = kt & 1;
+            if (kt + 1 < nk) stage((kt + 1) * GB_K, buf ^ 1);      // runs under this slab's MFMAs
+            const uint16_t* sA = smem + buf * (SA + SB);
+            const uint16_t* sB = sA + SA;
+#pragma unroll
+            for (int ks = 0; ks < GB_K / 16; ++ks) {
+                bf16x8 fa[2], fb[2];
+                const int c = 2 * ks + h;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int ra = wm + 32 * i + r, rb = wn + 32 * i + r;
+                    fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
+                    fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+            __syncthreads();                       // slab k+1 landed (DMA retired); slab k's buffer is free
+        }
+#pragma unroll
+        for (int g = 0; g < BM / EG; ++g) {
+            if (wm >= EG * g && wm < EG * (g + 1)) {   // C/D map: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int reg = 0; reg < 16; ++reg)
+                            sC[(wm - EG * g + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h) * GB_N + wn + 32 * j + r] =
+                                acc[i][j][reg];
+            }
+            gemm_finish<EPI, NT, EG>(sC, bias, R, C, m0 + EG * g, n0, N);
+        }
+    } else {
+        // 4 x 4 v_mfma_f32_16x16x32_bf16 per 32-deep step (lane l: A[l & 15][8 (l >> 4) + j])
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+        const int r = lane & 15, h = lane >> 4;
+        for (int kt = 0; kt < nk; ++kt) {
+            const int buf = kt & 1;
+            if (kt + 1 < nk) stage((kt + 1) * GB_K, buf ^ 1);
+            const uint16_t* sA = smem + buf * (SA + SB);
+            const uint16_t* sB = sA + SA;
+#pragma unroll
+            for (int ks = 0; ks < GB_K / 32; ++ks) {
+                bf16x8 fa[4], fb[4];
+                const int c = 4 * ks + h;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ra = wm + 16 * i + r, rb = wn + 16 * i + r;
+                    fa[i] = *reinterpret_cast<const bf16x8*>(sA + ra * GB_K + 8 * (c ^ (ra & 7)));
+                    fb[i] = *reinterpret_cast<const bf16x8*>(sB + rb * GB_K + 8 * (c ^ (rb & 7)));
+                }
+                if (GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int g = 0; g < BM / EG; ++g) {
+            if (wm >= EG * g && wm < EG * (g + 1)) {   // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg)
+                            sC[(wm - EG * g + 16 * i + 4 * h + reg) * GB_N + wn + 16 * j + r] = acc[i][j][reg];
+            }
+            gemm_finish<EPI, NT, EG>(sC, bias, R, C, m0 + EG * g, n0, N);
+        }
+    }
     (void)M;
 }
 
@@ -704,12 +834,12 @@ int ner_gemm(const void* A, const void* W, const void* bias, const void* resid, 
         // 256-row tiles when they still give every CU at least two tiles, else 128-row tiles
         const bool big = GEMM_BIG && M % 256 == 0 && (M / 256) * (N / GB_N) >= 512;
         if (big) {
-            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 256> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 256>
-                                                                                     : k_gemm2<EPI_BIAS, 256>;
+            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 256, GEMM_MF, GEMM_NB> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 256, GEMM_MF, GEMM_NB>
+                                                                                     : k_gemm2<EPI_BIAS, 256, GEMM_MF, GEMM_NB>;
             kern<<<(M / 256) * (N / GB_N), 512, 0, st>>>(a, w, b, rs, c, M, N, K);
         } else {
-            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 128> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 128>
-                                                                                     : k_gemm2<EPI_BIAS, 128>;
+            auto kern = epi == EPI_GELU ? k_gemm2<EPI_GELU, 128, GEMM_MF, GEMM_NB> : epi == EPI_RESID ? k_gemm2<EPI_RESID, 128, GEMM_MF, GEMM_NB>
+                                                                                     : k_gemm2<EPI_BIAS, 128, GEMM_MF, GEMM_NB>;
             kern<<<(M / 128) * (N / GB_N), 256, 0, st>>>(a, w, b, rs, c, M, N, K);
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;

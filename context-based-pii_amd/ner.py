@@ -33,9 +33,15 @@ _LIB = None
 
 
 def load_library(path: str = NER_LIB) -> ctypes.CDLL:
+    """the process-wide libner.so (loaded once; PII_NER_LIB selects another build)"""
     global _LIB
-    if _LIB is not None:
-        return _LIB
+    if _LIB is None:
+        _LIB = open_library(path)
+    return _LIB
+
+
+def open_library(path: str) -> ctypes.CDLL:
+    """a libner.so build with its signatures declared, not cached (A/B timing of several builds)"""
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} not built: run __graft_entry__.build() (no CPU fallback exists)")
     import torch  # noqa: F401  (one HIP runtime for torch and the library)
@@ -50,7 +56,6 @@ def load_library(path: str = NER_LIB) -> ctypes.CDLL:
     lib.ner_spans.argtypes = [P, I, P, P, P, I, I, I, I, P, P, P]
     for n in ("ner_gemm", "ner_layernorm", "ner_embed", "ner_attention", "ner_classify", "ner_tokenize", "ner_spans"):
         getattr(lib, n).restype = ctypes.c_int
-    _LIB = lib
     return lib
 
 
