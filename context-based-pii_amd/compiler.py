@@ -969,13 +969,13 @@ def plan_scan_groups(rules: Rules, budget: int, k_bytes: int) -> List[Tuple[List
 
     def split(pats):
         # the declared prefixes (dictionary types: DICT_SCAN_PREFIX) are worth a split -- they cut the
-        # candidate pairs several-fold -- so a set is halved before its prefixes are shortened, and a
-        # set with declared prefixes may take a WIDE table (one k_scan workgroup per CU); a set without
-        # them is halved until it fits the narrow limit (two workgroups per CU).  A single pattern whose
-        # automaton does not fit falls back to `budget` characters.
-        wide = any(p.scan_prefix for p in pats)
-        m = _scan_dfa(pats, budget, SCAN_WIDE_BYTES if wide else SCAN_GROUP_BYTES)
-        if fits(m, wide):
+        # candidate pairs several-fold -- so a set is halved before its prefixes are shortened.  A set
+        # whose automaton fits a WIDE table stays one group (one k_scan workgroup per CU: 352 us per
+        # pass at config 5 against 283 for a narrow pass, so one wide pass beats two narrow ones); only
+        # a set too large for that is halved.  A single pattern whose automaton does not fit falls back
+        # to `budget` characters.
+        m = _scan_dfa(pats, budget, SCAN_WIDE_BYTES)
+        if fits(m, True):
             out.append((pats, m))
             return
         if len(pats) == 1:
