@@ -8,6 +8,7 @@
 //   k_chunk_index  lane -> utterance ranges of ~BYTES_PER_LANE bytes (load balance, no halo needed);
 //                  per-row defaults
 //   k_lane_bits    utterance-start words per lane and 64-byte block (lane-interleaved, coalesced)
+//   k_halo         start states of the lanes a long row's slice boundaries cut (one workgroup per row)
 //   k_scan         REVERSE two-automaton DFA scan, tables in LDS.  D = relaxed detector prefilter,
 //                  K = exact context keywords.  Emits candidate STARTS (events) per lane
 //   k_pairs        agent-row context group (extract_expected_pii, main.py:558-578); (start, pattern)
@@ -182,6 +183,24 @@ __device__ __forceinline__ void row_lanes(const Geo& g, uint32_t r, uint32_t& ca
 // else -1) with coalesced stores, and lists the rows that will be cut (long rows).
 constexpr int CI_ROWS = 4;          // rows per thread in k_chunk_index (16-byte row-default stores)
 static_assert(CI_ROWS == 4, "k_chunk_index stores the row defaults as one uint4 / int4");
+// a row [s, e) (batch relative) that some slice boundary cuts (the test of g_cut)
+__device__ __forceinline__ bool cut_row(uint64_t s, uint64_t e, uint32_t r0, uint32_t lane_shift, uint32_t n_chunks,
+                                        uint32_t long_min) {
+    if (long_min == NO_CUTS || e - s <= long_min) return false;
+    const uint64_t kk = ((s + r0) >> lane_shift) + 1;                 // first boundary after its start
+    return kk < n_chunks && ((int64_t)(kk << lane_shift) - (int64_t)r0) < (int64_t)e;
+}
+
+// first_utt over the slices a cut row r spans, (slice of its start, slice of its end]: row r + 1
+__device__ __forceinline__ void fill_after(uint32_t* __restrict__ first_utt, uint32_t r, uint64_t s, uint64_t e,
+                                           uint32_t n_utt, uint32_t n_chunks, uint32_t lane_shift, uint32_t r0,
+                                           uint32_t t0, uint32_t step) {
+    const uint64_t c_lo = ((s + r0) >> lane_shift) + 1;
+    uint64_t c_hi = (r + 1 == n_utt) ? n_chunks : (e + r0) >> lane_shift;
+    if (c_hi > n_chunks) c_hi = n_chunks;
+    for (uint64_t c = c_lo + t0; c <= c_hi; c += step) first_utt[c] = r + 1;
+}
+
 __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict__ offs, const uint8_t* __restrict__ role,
                                                      uint32_t n_utt, uint32_t n_chunks, uint32_t lane_shift, uint32_t r0,
                                                      uint32_t long_min, int kw_always,
@@ -201,7 +220,7 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
 #pragma unroll
     for (int k = 0; k < CI_ROWS + 2; ++k) {
         const int64_t u = (int64_t)u0 - 1 + k;
-        o[k] = (u >= 0 && u <= (int64_t)n_utt) ? offs[u] : 0;
+        o[k] = (u >= 0 && u <= (int64_t)n_utt) ? offs[u] - base : 0;
     }
     uint32_t ol[CI_ROWS];
     int32_t kv[CI_ROWS];
@@ -209,26 +228,27 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
     for (int k = 0; k < CI_ROWS; ++k) {
         const uint32_t u = u0 + k;
         if (u > n_utt) break;
-        const uint64_t su = o[k + 1] - base + r0;
-        uint64_t c_lo = 0;
-        if (u > 0) c_lo = ((o[k] - base + r0) >> lane_shift) + 1;
-        uint64_t c_hi = (u == n_utt) ? n_chunks : su >> lane_shift;
-        if (c_hi > n_chunks) c_hi = n_chunks;
-        for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
+        // the slices after a CUT row are filled by k_fill_long, a workgroup per row (one thread storing a
+        // 1 MB row's 1024 entries serialised this kernel); the rest here
+        if (u == 0 || !cut_row(o[k], o[k + 1], r0, lane_shift, n_chunks, long_min)) {
+            const uint64_t c_lo = u > 0 ? ((o[k] + r0) >> lane_shift) + 1 : 0;
+            uint64_t c_hi = (u == n_utt) ? n_chunks : (o[k + 1] + r0) >> lane_shift;
+            if (c_hi > n_chunks) c_hi = n_chunks;
+            for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
+        }
         ol[k] = 0;
         kv[k] = -1;
         if (u < n_utt) {
-            const uint64_t len = o[k + 2] - o[k + 1];
-            ol[k] = (uint32_t)len;
+            ol[k] = (uint32_t)(o[k + 2] - o[k + 1]);
             kv[k] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
             if (wc_n) wc_n[u] = 0;
-            // a row that some slice boundary cuts (same test as g_cut)
-            if (long_min != NO_CUTS && len > long_min) {
-                const uint64_t kk = ((o[k + 1] - base + r0) >> lane_shift) + 1;      // first boundary after its start
-                if (kk < n_chunks && ((int64_t)(kk << lane_shift) - (int64_t)r0) < (int64_t)(o[k + 2] - base)) {
-                    const uint32_t at = atomicAdd(long_count, 1u);
-                    if (at < long_cap) long_rows[at] = u;
-                    else atomicOr(err, (uint32_t)ERR_STITCH);      // (sized by ensure_scratch: internal)
+            if (cut_row(o[k + 1], o[k + 2], r0, lane_shift, n_chunks, long_min)) {
+                const uint32_t at = atomicAdd(long_count, 1u);
+                if (at < long_cap) {
+                    long_rows[at] = u;
+                } else {
+                    atomicOr(err, (uint32_t)ERR_STITCH);      // (sized by ensure_scratch: internal)
+                    fill_after(first_utt, u, o[k + 1], o[k + 2], n_utt, n_chunks, lane_shift, r0, 0, 1);
                 }
             }
         }
@@ -243,6 +263,21 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
             out_len[u0 + k] = ol[k];
             kw[u0 + k] = kv[k];
         }
+    }
+}
+
+// first_utt over the slices of the listed cut rows (k_chunk_index left them), one workgroup per row
+__global__ __launch_bounds__(256) void k_fill_long(const uint64_t* __restrict__ offs, uint32_t n_utt,
+                                                   uint32_t n_chunks, uint32_t lane_shift, uint32_t r0,
+                                                   const uint32_t* __restrict__ long_rows,
+                                                   const uint32_t* __restrict__ long_count, uint32_t long_cap,
+                                                   uint32_t* __restrict__ first_utt) {
+    const uint32_t nrows = min(*long_count, long_cap);
+    const uint64_t base = offs[0];
+    for (uint32_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+        const uint32_t r = long_rows[ri];
+        fill_after(first_utt, r, offs[r] - base, offs[r + 1] - base, n_utt, n_chunks, lane_shift, r0, threadIdx.x,
+                   blockDim.x);
     }
 }
 
@@ -274,7 +309,7 @@ __device__ __forceinline__ uint32_t byte_c(const uint4& w) {
 constexpr int LANE_WORDS = 32;
 
 // exclusive end of the bytes lane L scans (a lane cut at hi starts from the state its halo produced,
-// k_lane_bits, instead of stepping the halo itself)
+// k_halo, instead of stepping the halo itself)
 __device__ __forceinline__ uint32_t scan_top(const Geo& g, const Lane& L) { return L.hi; }
 
 // bits of lane c's i-th block from the top (the slow path for i >= LANE_WORDS: binary search over the
@@ -396,28 +431,73 @@ __device__ __forceinline__ uint32_t lds_u16(uint32_t addr) {
 __device__ __forceinline__ uint32_t scan_state(uint32_t nd, uint32_t nk) { return (nd & 0xfffcu) | ((nk & 0xfffcu) << 16); }
 
 // The state a lane cut at hi starts from: both automata stepped right to left over the SCAN_HALO
-// bytes after the cut (clamped to the row) from the start state, tables read from global memory (a
-// cut lane is rare; k_scan_fix verifies the result against the neighbour's real state)
+// bytes after the cut (clamped to the row) from the start state, with the tables in LDS in k_scan's
+// layout (k_halo stages them); k_scan_fix verifies the result against the neighbour's real state.
+// The halo is read as aligned 16-byte chunks (each holds a batch byte, as k_scan's reads do), the
+// bytes taken from registers: per-byte loads from 64 lanes' distant rows thrashed L2.
 __device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* __restrict__ text, const Lane& L) {
     const uint32_t top = (uint32_t)min<int64_t>((int64_t)L.hi + SCAN_HALO, g_off(g, L.u1));
     const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)(R.SD * R.CDs / 2) * 4;
-    const uint8_t* tb = text + g.base;
+    const uintptr_t tb = (uintptr_t)(text + g.base);
     uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
-    for (int64_t b = (int64_t)top - 1; b >= (int64_t)L.hi; --b) {
-        const uint32_t x = R.cmap4[tb[b]];
-        const uint32_t ad = ((nd & ~pm & 0xfffcu) << R.dsh) + (x & 0xffffu);
-        const uint32_t ak = (nk & ~pm & 0xfffcu) + (R.SK > 1 ? (x >> 16) : tk_base);   // (groups >= 1: K stub)
-        nd = R.td[(ad - SCAN_TD_BASE) >> 1];
-        nk = R.tk[(ak - tk_base) >> 1];
-        pm = 0;
+    if (top <= L.hi) return scan_state(nd, nk);
+    const uintptr_t a_hi = (tb + top - 1) & ~(uintptr_t)15, a_lo = (tb + L.hi) & ~(uintptr_t)15;
+    for (uintptr_t a = a_hi;; a -= 16) {
+        const uint4 w = gload16(a);
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 15; j >= 0; --j) {
+            const uintptr_t b = a + (uintptr_t)j;
+            if (b >= tb + L.hi && b < tb + top) {
+                const uint32_t x = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+                    (size_t)(4u * ((wd[j >> 2] >> (8 * (j & 3))) & 0xffu)));
+                const uint32_t ad = ((nd & ~pm & 0xfffcu) << R.dsh) + (x & 0xffffu);
+                const uint32_t ak = (nk & ~pm & 0xfffcu) + (R.SK > 1 ? (x >> 16) : tk_base);   // (groups >= 1: K stub)
+                nd = lds_u16(ad);
+                nk = lds_u16(ak);
+                pm = 0;
+            }
+        }
+        if (a == a_lo) break;
     }
     return scan_state(nd, nk);
 }
 
+// Halo states of every cut lane, one workgroup per long row (the k_scan_fix grid), the group's scan
+// tables staged in LDS: the lanes (ca, kb] continue long row r, so lanes [ca, kb) are cut at hi.
+// Only long rows have cut lanes, so a batch without them costs one early exit.
+__global__ __launch_bounds__(256) void k_halo(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+                                              const uint32_t* __restrict__ long_rows,
+                                              const uint32_t* __restrict__ long_count,
+                                              uint32_t* __restrict__ lane_st, const uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+    const uint32_t nrows = *long_count;
+    if (blockIdx.x >= nrows || (*err & (ERR_ARGS | ERR_STITCH))) return;
+    {
+        const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
+        const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
+        const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
+        uint32_t* d_td = smem32 + SCAN_TD_BASE / 4;
+        uint32_t* d_tk = d_td + nd_words;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
+        for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
+        for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
+    }
+    __syncthreads();
+    for (uint32_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+        uint32_t ca, kb;
+        int64_t s_r, e_r;
+        row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
+        for (uint32_t c = ca + threadIdx.x; c < kb; c += blockDim.x) {
+            const Lane L = g_lane(g, c);
+            if (L.chi && scan_top(g, L) > L.lo) lane_st[2 * c] = halo_state(R, g, text, L);
+        }
+    }
+}
+
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
-__global__ __launch_bounds__(256) void k_lane_bits(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
-                                                   const uint32_t* __restrict__ lane_pos,
-                                                   uint64_t* __restrict__ words, uint32_t* __restrict__ lane_st) {
+__global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* __restrict__ lane_pos,
+                                                   uint64_t* __restrict__ words) {
     __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -436,8 +516,6 @@ __global__ __launch_bounds__(256) void k_lane_bits(const RulesDev R, const Geo g
     const Lane L = g_lane(g, c);
     const uint32_t top = scan_top(g, L);
     if (top <= L.lo) return;
-    if (L.chi) lane_st[2 * c] = halo_state(R, g, text, L);
-    if (!words) return;                      // SCAN groups >= 1: only their halo states
     const int64_t b_hi = ((int64_t)top - 1 + g.r0) >> 6, b_lo = ((int64_t)L.lo + g.r0) >> 6;
     const int64_t nw = min<int64_t>(b_hi - b_lo + 1, LANE_WORDS);
     const uint32_t slot = lane_pos[c];
@@ -4271,6 +4349,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                                                 e->out_len, e->kw, win_ctx ? e->wc_n : nullptr,
                                                                 e->long_rows, e->long_count, (uint32_t)e->cap_long, base,
                                                                 total_bytes, e->d_err);
+        if (e->long_min != NO_CUTS)
+            k_fill_long<<<row_grid(e, total_bytes), 256, 0, st>>>(offs, n_utt, n_chunks, e->lane_shift, e->r0, e->long_rows,
+                                                                   e->long_count, (uint32_t)e->cap_long, e->first_utt);
         if (n_chunks > 0) {
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
@@ -4285,8 +4366,10 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 Event* evq = e->ev + (uint64_t)q * e->cap_ev;
                 uint32_t* cq = e->lane_cnt + (uint64_t)q * e->cap_lanes;
                 uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
-                k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(Rq, g, text, e->lane_pos,
-                                                                     q == 0 ? e->bnd : nullptr, stq);
+                if (q == 0) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
+                if (e->long_min != NO_CUTS)
+                    k_halo<<<row_grid(e, total_bytes), 256, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
+                                                                                  e->long_count, stq, e->d_err);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
                 const int nt = Rq.dsh ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
                 (q == 0 ? k_scan<true> : Rq.dsh ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
@@ -5135,7 +5218,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
          hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
          hipFuncSetAttribute((const void*)k_scan<false, SCAN_BLOCK_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)max_lds) != hipSuccess))
+                             (int)max_lds) != hipSuccess ||
+         hipFuncSetAttribute((const void*)k_halo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) != hipSuccess))
         return fail("cannot raise LDS limit");
     if (max_lds + FIX_LDS > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_scan_fix, hipFuncAttributeMaxDynamicSharedMemorySize,
