@@ -442,8 +442,10 @@ __device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* _
     uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
     if (top <= L.hi) return scan_state(nd, nk);
     const uintptr_t a_hi = (tb + top - 1) & ~(uintptr_t)15, a_lo = (tb + L.hi) & ~(uintptr_t)15;
+    uint4 nx = gload16(a_hi);
     for (uintptr_t a = a_hi;; a -= 16) {
-        const uint4 w = gload16(a);
+        const uint4 w = nx;
+        if (a > a_lo) nx = gload16(a - 16);                // the next chunk's load runs under these steps
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int j = 15; j >= 0; --j) {
@@ -466,7 +468,8 @@ __device__ uint32_t halo_state(const RulesDev& R, const Geo& g, const uint8_t* _
 // Halo states of every cut lane, one workgroup per long row (the k_scan_fix grid), the group's scan
 // tables staged in LDS: the lanes (ca, kb] continue long row r, so lanes [ca, kb) are cut at hi.
 // Only long rows have cut lanes, so a batch without them costs one early exit.
-__global__ __launch_bounds__(256) void k_halo(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+constexpr int HALO_BLOCK = 1024;    // k_halo: lanes of a long row in flight per workgroup (one per CU)
+__global__ __launch_bounds__(HALO_BLOCK) void k_halo(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                               const uint32_t* __restrict__ long_rows,
                                               const uint32_t* __restrict__ long_count,
                                               uint32_t* __restrict__ lane_st, const uint32_t* __restrict__ err) {
@@ -2364,18 +2367,34 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
                                                  const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & (ERR_ABORT | ERR_STITCH)) return;
+    // the row's chain starts are compacted first, so the chains run side by side (a thread per lane
+    // left most threads idle and ran the few chains of a row one slice of 256 lanes after another)
+    constexpr uint32_t FIX_CAP = 1024;
+    __shared__ uint32_t s_chain[FIX_CAP];
+    __shared__ uint32_t s_nc;
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const SelTabs Tb = sel_tabs(lb, li);
+    auto run = [&](uint32_t j) {
+        uint32_t c = j + 1;
+        while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
+        select_run<EXT>(R, Tb, g, io, j, c);
+    };
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         uint32_t ca, kb;
         int64_t s_r, e_r;
         row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
+        __syncthreads();
+        if (threadIdx.x == 0) s_nc = 0;
+        __syncthreads();
         for (uint32_t j = ca + threadIdx.x; j < kb; j += blockDim.x) {
             if (dirty[j] || !dirty[j + 1]) continue;
-            uint32_t c = j + 1;
-            while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
-            select_run<EXT>(R, Tb, g, io, j, c);
+            const uint32_t at = atomicAdd(&s_nc, 1u);
+            if (at < FIX_CAP) s_chain[at] = j;
+            else run(j);
         }
+        __syncthreads();
+        const uint32_t n = min(s_nc, FIX_CAP);
+        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) run(s_chain[k]);
     }
 }
 
@@ -4368,7 +4387,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
                 if (q == 0) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
                 if (e->long_min != NO_CUTS)
-                    k_halo<<<row_grid(e, total_bytes), 256, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
+                    k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
                 const int nt = Rq.dsh ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
