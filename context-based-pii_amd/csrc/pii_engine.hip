@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
 #pragma unroll
     for (int k = 0; k < CI_ROWS + 2; ++k) {
         const int64_t u = (int64_t)u0 - 1 + k;
-        o[k] = (u >= 0 && u <= (int64_t)n_utt) ? offs[u] - base : 0;
+        o[k] = (u >= 0 && u <= (int64_t)n_utt) ? offs[u] : 0;
     }
     uint32_t ol[CI_ROWS];
     int32_t kv[CI_ROWS];
@@ -230,25 +230,27 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
         if (u > n_utt) break;
         // the slices after a CUT row are filled by k_fill_long, a workgroup per row (one thread storing a
         // 1 MB row's 1024 entries serialised this kernel); the rest here
-        if (u == 0 || !cut_row(o[k], o[k + 1], r0, lane_shift, n_chunks, long_min)) {
-            const uint64_t c_lo = u > 0 ? ((o[k] + r0) >> lane_shift) + 1 : 0;
-            uint64_t c_hi = (u == n_utt) ? n_chunks : (o[k + 1] + r0) >> lane_shift;
+        if (u == 0 || o[k + 1] - o[k] <= long_min ||
+            !cut_row(o[k] - base, o[k + 1] - base, r0, lane_shift, n_chunks, long_min)) {
+            const uint64_t c_lo = u > 0 ? ((o[k] - base + r0) >> lane_shift) + 1 : 0;
+            uint64_t c_hi = (u == n_utt) ? n_chunks : (o[k + 1] - base + r0) >> lane_shift;
             if (c_hi > n_chunks) c_hi = n_chunks;
             for (uint64_t c = c_lo; c <= c_hi; ++c) first_utt[c] = u;
         }
         ol[k] = 0;
         kv[k] = -1;
         if (u < n_utt) {
-            ol[k] = (uint32_t)(o[k + 2] - o[k + 1]);
+            const uint64_t len = o[k + 2] - o[k + 1];
+            ol[k] = (uint32_t)len;
             kv[k] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
             if (wc_n) wc_n[u] = 0;
-            if (cut_row(o[k + 1], o[k + 2], r0, lane_shift, n_chunks, long_min)) {
+            if (len > long_min && cut_row(o[k + 1] - base, o[k + 2] - base, r0, lane_shift, n_chunks, long_min)) {
                 const uint32_t at = atomicAdd(long_count, 1u);
                 if (at < long_cap) {
                     long_rows[at] = u;
                 } else {
                     atomicOr(err, (uint32_t)ERR_STITCH);      // (sized by ensure_scratch: internal)
-                    fill_after(first_utt, u, o[k + 1], o[k + 2], n_utt, n_chunks, lane_shift, r0, 0, 1);
+                    fill_after(first_utt, u, o[k + 1] - base, o[k + 2] - base, n_utt, n_chunks, lane_shift, r0, 0, 1);
                 }
             }
         }
@@ -2366,10 +2368,10 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
                                                  const uint32_t* __restrict__ long_count,
                                                  const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
-    if (*err & (ERR_ABORT | ERR_STITCH)) return;
+    if ((*err & (ERR_ABORT | ERR_STITCH)) || blockIdx.x >= *long_count) return;     // (before the image load)
     // the row's chain starts are compacted first, so the chains run side by side (a thread per lane
     // left most threads idle and ran the few chains of a row one slice of 256 lanes after another)
-    constexpr uint32_t FIX_CAP = 1024;
+    constexpr uint32_t FIX_CAP = 256;
     __shared__ uint32_t s_chain[FIX_CAP];
     __shared__ uint32_t s_nc;
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
