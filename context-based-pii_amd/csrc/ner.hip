@@ -830,7 +830,12 @@ int ner_gemm(const void* A, const void* W, const void* bias, const void* resid, 
     uint16_t* c = static_cast<uint16_t*>(C);
     const float* b = static_cast<const float*>(bias);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (GEMM_PIPE) {
+    // k_gemm2 (two slab buffers, two workgroups per CU) while the tile count is a few rounds of the
+    // chip's workgroup slots; past that (the NER on the redaction path: M = 524288 tokens) the
+    // single-buffer k_gemm's 3-4 workgroups per CU hide the DMA better (QKV 759 vs 647 TFLOP/s there,
+    // 597 vs 634 at M = 8192; tools/gemm_ab.py, GEMM_M)
+    const long tiles = (long)(M / GB_M) * (N / GB_N);
+    if (GEMM_PIPE && tiles <= 16L * 256) {
         // 256-row tiles when they still give every CU at least two tiles, else 128-row tiles
         const bool big = GEMM_BIG && M % 256 == 0 && (M / 256) * (N / GB_N) >= 512;
         if (big) {

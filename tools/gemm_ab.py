@@ -13,14 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "context-based-pii_amd"))
 import ner  # noqa: E402
 
-SHAPES = [("qkv", 8192, 2304, 768, 0), ("out", 8192, 768, 768, 2), ("ffn1", 8192, 3072, 768, 1),
-          ("ffn2", 8192, 768, 3072, 2)]
+TOKENS = int(os.environ.get("GEMM_M", "8192"))     # 64 x 128 tokens (bench --workload ner); 524288 = ner-redact
+SHAPES = [("qkv", TOKENS, 2304, 768, 0), ("out", TOKENS, 768, 768, 2), ("ffn1", TOKENS, 3072, 768, 1),
+          ("ffn2", TOKENS, 768, 3072, 2)]
 
 
 ROUNDS = 5
 
 
-def timeit(fn, reps=50):
+def timeit(fn, reps=max(3, 50 * 8192 // TOKENS)):
     for _ in range(5):
         fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
