@@ -25,7 +25,7 @@ import time
 from concurrent.futures import Future
 from typing import List, Optional, Tuple
 
-from .service import PiiService
+from .service import PartialBatchError, PiiService
 
 
 class MicroBatcher:
@@ -77,10 +77,16 @@ class MicroBatcher:
                 res = self.service.process_requests([(k, d) for k, d, _ in batch])
                 for (_, _, f), r in zip(batch, res):
                     f.set_result(r)
-            except Exception:
-                # a failure that request validation did not foresee: rerun the batch one request at
-                # a time so that only the request that raises fails (as it would alone in the
-                # reference's per-request handler), and never leave a request thread waiting
+            except Exception as exc:
+                # a failure that request validation did not foresee: the requests whose sub-batch
+                # completed keep their responses (their context is committed: running them again
+                # would store it twice); the rest run one at a time, so that only the request that
+                # raises fails (as it would alone in the reference's per-request handler), and no
+                # request thread is left waiting
+                done = exc.done if isinstance(exc, PartialBatchError) else {}
+                for i, (_, _, f) in enumerate(batch):
+                    if i in done and not f.done():
+                        f.set_result(done[i])
                 for k, d, f in batch:
                     if f.done():
                         continue

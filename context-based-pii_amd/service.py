@@ -81,6 +81,16 @@ def _dec(b: bytes) -> str:
     return b.decode("utf-8", "surrogateescape")
 
 
+class PartialBatchError(Exception):
+    """process_requests raised in a sub-batch after earlier sub-batches had committed: `done` maps
+    request index -> response for every request that completed (and must not run again)."""
+
+    def __init__(self, done: Dict[int, Tuple[dict, int]], cause: Exception):
+        super().__init__(f"{type(cause).__name__}: {cause}")
+        self.done = done
+        self.cause = cause
+
+
 class SlotMap:
     """conversation_id -> engine context slot (the Redis key ``context:{conversation_id}`` -> its HBM
     record); slot 0 is reserved for stateless calls.
@@ -388,8 +398,20 @@ class PiiService:
             split.append(cut)
             if kind == "agent":
                 agents.add(cid)
+        committed = False
         for run in self._sub_batches([reqs[i][1]["conversation_id"] for i in valid], split):
-            self._run_requests(reqs, [valid[j] for j in run], out)
+            idx = [valid[j] for j in run]
+            try:
+                self._run_requests(reqs, idx, out)
+            except Exception as e:
+                if not committed:
+                    raise
+                # earlier sub-batches are committed (their context is stored): report them, so a
+                # caller re-runs only the requests that did not complete
+                failed = set(idx)
+                done = {i: r for i, r in enumerate(out) if r is not None and i not in failed}
+                raise PartialBatchError(done, e) from e
+            committed = True
         return out
 
     def _run_requests(self, reqs, idxs: List[int], out) -> None:

@@ -5,6 +5,7 @@ CPU tests drive PiiService with a test double of the engine whose results come f
 (test infrastructure only); the `gpu` tests drive it with the real HIP engine and compare the whole
 handler sequence with the oracle's replay of the reference handlers (main.py:344-466)."""
 import json
+import time
 import os
 
 import numpy as np
@@ -564,6 +565,45 @@ def test_malformed_request_fails_alone(oracle_cfg):
                 res.append("raised")
     mb.close()
     assert res[1] == "raised" and res[0][1] == 200 and res[2][1] == 200
+
+
+def test_microbatch_failure_after_a_committed_sub_batch_runs_nothing_twice(oracle_cfg):
+    """A micro-batch splits into engine calls (a realtime request after an agent request of its
+    conversation starts a new one).  When a later call raises, the earlier call's requests are
+    committed -- the agent's context is stored -- so the batcher answers them from the partial
+    result and re-runs only the failed rest (running them again stored contexts twice)."""
+    S = pkg("service")
+    svc = S.PiiService(engine=OracleEngine(oracle_cfg, n_slots=32), clock=Clock())
+    real = svc._run
+    agent_text = b"What is your email address?"
+    runs = {"agent": 0}
+
+    def flaky(texts, *a):
+        if any(agent_text == t for t in texts):
+            runs["agent"] += 1
+        if any(b"boom" in t for t in texts):
+            raise RuntimeError("unforeseen")
+        return real(texts, *a)
+    svc._run = flaky
+    reqs = [("agent", {"conversation_id": "c1", "transcript": agent_text.decode()}),
+            ("realtime", {"conversation_id": "c1", "utterance": "boom"})]
+    with pytest.raises(S.PartialBatchError) as ei:
+        svc.process_requests(reqs)
+    assert set(ei.value.done) == {0} and ei.value.done[0][1] == 200
+    assert runs["agent"] == 1
+    A = pkg("app")
+    mb = A.MicroBatcher(svc, max_wait_s=0.05)
+    import concurrent.futures as cf
+    runs["agent"] = 0
+    with cf.ThreadPoolExecutor(2) as ex:
+        f0 = ex.submit(mb.submit, *reqs[0])
+        time.sleep(0.005)
+        f1 = ex.submit(mb.submit, *reqs[1])
+        r0 = f0.result()
+        with pytest.raises(RuntimeError):
+            f1.result()
+    mb.close()
+    assert r0[1] == 200 and runs["agent"] == 1
 
 
 @pytest.mark.gpu
