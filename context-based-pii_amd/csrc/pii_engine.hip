@@ -38,6 +38,7 @@ using namespace pii;
 namespace {
 
 constexpr int NE_MAX = 2;          // excluder patterns
+constexpr size_t SCAN_LDS_TWO_WG = 80 * 1024;   // k_scan tables up to this: two workgroups per CU
 constexpr int SCAN_BLOCK = 768;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
 constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
 constexpr int SCAN_ITEMS = 8;      // items per thread in the offset scans (blocked, 16-byte accesses)
@@ -4392,8 +4393,12 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
-                const int nt = Rq.dsh ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
-                (q == 0 ? k_scan<true> : Rq.dsh ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
+                // a WIDE table (row offsets / 2) that still leaves room for two workgroups per CU runs
+                // at 768 threads too: 6 waves/SIMD instead of 4 (config 5: the 262 regex types' 70 KB
+                // table); only the dictionary groups' ~100 KB tables need one 1024-thread workgroup
+                const bool one_wg = e->sg_lds[q] > SCAN_LDS_TWO_WG;
+                const int nt = one_wg ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
+                (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
                     (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], st>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
                 if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
