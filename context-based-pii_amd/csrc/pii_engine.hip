@@ -1863,7 +1863,9 @@ __device__ __forceinline__ int pair_lik(const EvalTabs& E, int T, const uint8_t*
 }
 
 // per matched pair: validator + hotword windows of the row's context variant -> likelihood
-template <bool GI>
+// RG: the image omits the per-(variant, type) rule lists (config 5's are 107 KB: with them the image
+// leaves room for one 1024-thread workgroup per CU); they are read from global memory (L2) instead
+template <bool GI, bool RG = false>
 __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
                                                           const uint8_t* __restrict__ text0,
                                                           const uint64_t* __restrict__ offs,
@@ -1874,10 +1876,16 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
                                                           const uint32_t* __restrict__ mcount, uint32_t nseg,
                                                           const EvLoc* __restrict__ evloc,
                                                           const int32_t* __restrict__ pend,
-                                                          const PairRes* __restrict__ pres, SelRec* __restrict__ sel) {
+                                                          const PairRes* __restrict__ pres, SelRec* __restrict__ sel,
+                                                          const uint32_t* __restrict__ g_roff,
+                                                          const uint16_t* __restrict__ g_rids) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
-    const EvalTabs E = eval_tabs(lb, li);
+    EvalTabs E = eval_tabs(lb, li);
+    if (RG) {
+        E.roff = g_roff;
+        E.rids = g_rids;
+    }
     const uint8_t* text = text0 + offs[0];
     __shared__ uint32_t s_mp[PAIR_WAVES + 1];
     const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg * PAIR_WAVES);
@@ -1979,6 +1987,10 @@ struct SelIO {
     const uint32_t* ext_n;
     uint32_t ext_stride;
     uint32_t* err;          // ERR_EXT: a malformed external span
+    // the per-(variant, type) exclusion lists in global memory (L2) when the LDS image omits them
+    // (config 5's are 93 KB: with them k_select held one 256-thread workgroup per CU); else null
+    const uint32_t* g_xoff;
+    const uint16_t* g_xids;
 };
 
 __device__ __forceinline__ uint64_t fd_base(const Lane& L, uint32_t c, int min_len) {
@@ -2304,7 +2316,11 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & ERR_ABORT) return;           // the batch is re-run with a larger queue
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
-    const SelTabs Tb = sel_tabs(lb, li);
+    SelTabs Tb = sel_tabs(lb, li);
+    if (io.g_xoff) {
+        Tb.xoff = io.g_xoff;
+        Tb.xids = io.g_xids;
+    }
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= g.n_chunks) return;
     select_run<EXT>(R, Tb, g, io, c, c);
@@ -2376,7 +2392,11 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
     __shared__ uint32_t s_chain[FIX_CAP];
     __shared__ uint32_t s_nc;
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
-    const SelTabs Tb = sel_tabs(lb, li);
+    SelTabs Tb = sel_tabs(lb, li);
+    if (io.g_xoff) {
+        Tb.xoff = io.g_xoff;
+        Tb.xids = io.g_xids;
+    }
     auto run = [&](uint32_t j) {
         uint32_t c = j + 1;
         while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
@@ -3932,6 +3952,7 @@ bool parse_blob(const uint8_t* p, size_t n, std::vector<Section>& out) {
 
 // ================================================================================ engine object
 constexpr size_t IMG_LDS_MAX = 160 * 1024;
+constexpr size_t IMG_LDS_SPLIT = 80 * 1024;    // pair-kernel image size past which its per-(variant, type) lists stay in L2
 struct DevImage {
     LdsImage li{};
     uint4* d = nullptr;
@@ -3976,6 +3997,8 @@ struct pii_engine {
     AccTabs acct{};
     uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs<.., MULTI>)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
+    DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
+    DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
     int n_cu = 256;
     // persistent state (replaces Redis)
     int32_t* st_group = nullptr;
@@ -4516,21 +4539,31 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                            st, wf ? wf->err_init : nullptr, wf == nullptr)))
         return rc;
     if (n_utt > 0 && n_chunks > 0) {
-        (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
-                                                                         st>>>(
-            e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
-            e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont));
+        if (e->img_eval_rg.d) {
+            k_pair_eval<false, true><<<e->n_seg, PAIR_BLOCK, e->img_eval_rg.lds(), st>>>(
+                e->img_eval_rg.d, e->img_eval_rg.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
+                e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), R.rule_off,
+                R.rule_ids);
+        } else {
+            (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
+                                                                             st>>>(
+                e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
+                e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), nullptr, nullptr);
+        }
+        const bool xg = e->img_sel_rg.d != nullptr;
+        const DevImage& isel = xg ? e->img_sel_rg : e->img_sel;
         const SelIO io{e->lane_pair, e->lane_np, reinterpret_cast<const SelRec*>(e->cont), e->pend, e->pair_cap, role, ctx, e->fd,
-                       e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill, ext, ext_n, ext_stride, e->d_err};
-        const bool gi = e->img_sel.global;
+                       e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill, ext, ext_n, ext_stride, e->d_err,
+                       xg ? R.excl_off : nullptr, xg ? R.excl_ids : nullptr};
+        const bool gi = isel.global;
         auto ksel = has_ext ? (gi ? k_select<true, true> : k_select<false, true>)
                             : (gi ? k_select<true, false> : k_select<false, false>);
         auto kfix = has_ext ? (gi ? k_sel_fix<true, true> : k_sel_fix<false, true>)
                             : (gi ? k_sel_fix<true, false> : k_sel_fix<false, false>);
-        ksel<<<(n_chunks + 255) / 256, 256, e->img_sel.lds(), st>>>(Rsel, e->img_sel.d, e->img_sel.li, g, io, e->d_err);
+        ksel<<<(n_chunks + 255) / 256, 256, isel.lds(), st>>>(Rsel, isel.d, isel.li, g, io, e->d_err);
         const uint32_t rg = row_grid(e, total_bytes);
         k_sel_dirty<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_reach, e->dirty, e->d_err);
-        kfix<<<rg, 256, e->img_sel.lds(), st>>>(Rsel, e->img_sel.d, e->img_sel.li, g, io, e->long_rows, e->long_count,
+        kfix<<<rg, 256, isel.lds(), st>>>(Rsel, isel.d, isel.li, g, io, e->long_rows, e->long_count,
                                                  e->dirty, e->d_err);
         k_rowlen<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_rd, e->lane_rowbase, e->out_len,
                                           e->d_err);
@@ -5189,6 +5222,29 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
             return fail("rule table upload failed");
+        if (e->img_eval.li.total > IMG_LDS_SPLIT) {
+            auto pr = pe;
+            pr[EV_ROFF] = std::make_pair((const void*)nullptr, (size_t)0);
+            pr[EV_RIDS] = std::make_pair((const void*)nullptr, (size_t)0);
+            if (!make_image(pr, e->img_eval_rg)) return fail("rule table upload failed");
+            if (e->img_eval_rg.global || (e->img_eval_rg.li.total > 64 * 1024 &&
+                                          hipFuncSetAttribute((const void*)k_pair_eval<false, true>,
+                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                              (int)e->img_eval_rg.li.total) != hipSuccess)) {
+                (void)hipFree(e->img_eval_rg.d);
+                e->img_eval_rg = DevImage{};
+            }
+        }
+        if (e->img_sel.li.total > IMG_LDS_SPLIT) {
+            auto pr = ps;
+            pr[SE_XOFF] = std::make_pair((const void*)nullptr, (size_t)0);
+            pr[SE_XIDS] = std::make_pair((const void*)nullptr, (size_t)0);
+            if (!make_image(pr, e->img_sel_rg)) return fail("rule table upload failed");
+            if (e->img_sel_rg.global || e->img_sel_rg.li.total > 64 * 1024) {      // (no gain: keep the full image)
+                (void)hipFree(e->img_sel_rg.d);
+                e->img_sel_rg = DevImage{};
+            }
+        }
         // (the window re-scan's kernels read an image past LDS in place, like the pair kernels)
         const std::pair<const void*, const DevImage*> big[] = {
             {(const void*)k_pair_first<false>, &e->img_first}, {(const void*)k_pair_eval<false>, &e->img_eval},
@@ -5287,7 +5343,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->ev, e->fd, e->n_ev, e->n_find,
                     e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
-                    e->img_first.d, e->img_eval.d, e->img_sel.d, e->kw, e->ctx, e->agg_v, e->commit,
+                    e->img_first.d, e->img_eval.d, e->img_eval_rg.d, e->img_sel.d, e->img_sel_rg.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
