@@ -38,6 +38,9 @@ using namespace pii;
 namespace {
 
 constexpr int NE_MAX = 2;          // excluder patterns
+#ifndef SCAN_INLINE_HALO
+#define SCAN_INLINE_HALO 1          // k_scan steps a cut lane's halo itself (no k_halo launch per SCAN group)
+#endif
 constexpr size_t SCAN_LDS_TWO_WG = 80 * 1024;   // k_scan tables up to this: two workgroups per CU
 constexpr int SCAN_BLOCK = 768;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
 constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
@@ -724,7 +727,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
         // "previous byte started an utterance": start rows; a lane cut at hi continues from its halo state
         uint32_t nd = 0, nk = 0, pm = 0xffffffffu;
         if (L.chi) {
+#if SCAN_INLINE_HALO
+            // the lane's start state: its halo stepped here, from the tables already in LDS (a cut
+            // lane is rare except in long rows, where every lane pays 128 of its 1024 steps); the
+            // guess is kept for k_scan_fix, which checks it against the neighbour's real end state
+            const uint32_t hs = halo_state(R, g, text, L);
+            lane_st[2 * c] = hs;
+#else
             const uint32_t hs = lane_st[2 * c];
+#endif
             nd = hs & 0xffffu;
             nk = hs >> 16;
             pm = 0;
@@ -4412,7 +4423,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 uint32_t* cq = e->lane_cnt + (uint64_t)q * e->cap_lanes;
                 uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
                 if (q == 0) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
-                if (e->long_min != NO_CUTS)
+                if (!SCAN_INLINE_HALO && e->long_min != NO_CUTS)
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
                 if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
