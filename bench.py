@@ -347,9 +347,9 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
     Bw = n_bytes + ob + 8 * (n + 1) * 2 + 5 * n + 16 * ns
     t_pipe = max(per_stage[5], 1e-9) / 1e3
     # dominant kernel k_scan, algorithmic bytes per launch (DESIGN.md "Roofline accounting"):
-    # every utterance byte once + every utterance's start offset (8 B; the lane walks them down with
-    # its blocks) + per lane its first_utt pair, offsets pair, event count (24 B) + 8 B per event
-    scan_B = n_bytes + 8 * n + 24 * n_lanes + 8 * n_events
+    # every utterance byte once + the utterance-start bitmap (1 bit per byte) + per lane its
+    # first_utt pair, offsets pair, event count (24 B) + 8 B per event written
+    scan_B = n_bytes + (n_bytes + 63) // 64 * 8 + 24 * n_lanes + 8 * n_events
     scan_GBps = scan_B / max(k_ms["k_scan"] / 1e3, 1e-12) / 1e9
     # k_redact: what it moves -- the input bytes, the output bytes, one 16-B RSpan per kept span and
     # the 4-B first-span index per 64 KiB output tile (no offsets / counts, it reads none)

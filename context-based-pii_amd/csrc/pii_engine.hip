@@ -682,11 +682,8 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 // row stays the start row, its transition is the stub's class-0 entry), one LDS read less per byte
 // NT: 768 threads (two workgroups per CU with tables <= 80 KiB, 6 waves / SIMD), or SCAN_BLOCK_WIDE for
 // a WIDE group's table (one workgroup per CU: 16 waves instead of 12)
-// WB: the utterance-start bits come from k_lane_bits' words (a rule set of several SCAN groups: one
-// k_lane_bits pass for all of them; each group walking the offsets itself cost ~70 us per group at
-// config 5), else each lane walks its utterances' offsets itself (one group: no k_lane_bits pass)
 constexpr int SCAN_BLOCK_WIDE = 1024;
-template <bool HK, int NT = SCAN_BLOCK, bool WB = false>
+template <bool HK, int NT = SCAN_BLOCK>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? 6 : 4, NT == SCAN_BLOCK ? 6 : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
@@ -755,55 +752,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
         if (4 * bb_hi + 1 <= q_end) n1 = gload16(tpb + (uintptr_t)bb_hi * 64u + 16);
         if (4 * bb_hi + 2 <= q_end) n2 = gload16(tpb + (uintptr_t)bb_hi * 64u + 32);
         if (4 * bb_hi + 3 <= q_end) n3 = gload16(tpb + (uintptr_t)bb_hi * 64u + 48);
-        // utterance-start bits of the block.  WB: from the k_lane_bits words (several SCAN groups share
-        // them).  Otherwise made here as the blocks go down: x = start + r0 + 64 of the lane's next
-        // utterance not yet placed (its block + 1 = x >> 6; 0 once none is left), one offsets load per
-        // utterance, the start after it (xn) loaded one utterance ahead so that a block's test waits on a
-        // load issued an utterance earlier.  An empty row shares its position with the next row's start
-        // or the lane's top, so its bit is that one; the top bit seeds the first block.
-        uint64_t nb = 0, bits = 0;
-        int32_t v = 0, vmin = 0;
-        uint32_t x = 0, xn = 0;
-        if (WB) {
-            nb = words[t];
-        } else {
-            v = (int32_t)L.u1 - 1;
-            vmin = (int32_t)(L.u0 + (L.clo ? 1u : 0u));
-            x = v >= vmin ? (uint32_t)g_off(g, (uint32_t)v) + r0 + 64u : 0u;
-            xn = v > vmin ? (uint32_t)g_off(g, (uint32_t)(v - 1)) + r0 + 64u : 0u;
-            const uint32_t dt = top + r0 - 64u * bb_hi;
-            if (!L.chi && dt < 64u) bits = 1ull << dt;
-        }
+        uint64_t nb = words[t];
         for (uint32_t bb = bb_hi;; --bb) {
-            if (WB) {
-                bits = nb;
-            } else {
-                while ((x >> 6) > bb) {
-                    const uint32_t d = x - 64u - 64u * bb;
-                    if (d < 64u) bits |= 1ull << d;
-                    x = xn;
-                    --v;
-                    xn = v > vmin ? (uint32_t)g_off(g, (uint32_t)(v - 1)) + r0 + 64u : 0u;
-                }
-            }
             const uint4 w0 = n0, w1 = n1, w2 = n2, w3 = n3;
+            const uint64_t bits = nb;
             if (bb > bb_lo) {
                 const uintptr_t q = tpb + (uintptr_t)(bb - 1) * 64u;
                 n0 = gload16(q);
                 n1 = gload16(q + 16);
                 n2 = gload16(q + 32);
                 n3 = gload16(q + 48);
-                if (WB) {
-                    const uint32_t i = bb_hi - (bb - 1);
-                    nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * g.n_chunks + t] : block_bits_slow(g, c, i);
-                }
+                const uint32_t i = bb_hi - (bb - 1);
+                nb = i < (uint32_t)LANE_WORDS ? words[(uint64_t)i * g.n_chunks + t] : block_bits_slow(g, c, i);
             }
             const uint32_t bpos = 64u * bb - r0;        // relative position of the block's byte 0 (mod 2^32)
             SCAN_SUB(w3, 48)
             SCAN_SUB(w2, 32)
             SCAN_SUB(w1, 16)
             SCAN_SUB(w0, 0)
-            if (!WB) bits = 0;
             if (bb == bb_lo) break;
         }
         if (L.clo) lane_st[2 * c + 1] = scan_state(nd, nk);        // lo is block aligned: state after byte lo
@@ -4457,8 +4423,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 Event* evq = e->ev + (uint64_t)q * e->cap_ev;
                 uint32_t* cq = e->lane_cnt + (uint64_t)q * e->cap_lanes;
                 uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
-                const bool wb = e->n_sg > 1;          // (one group: each lane walks its offsets itself)
-                if (q == 0 && wb) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
+                if (q == 0) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
                 if (!SCAN_INLINE_HALO && e->long_min != NO_CUTS)
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
@@ -4468,9 +4433,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 // table); only the dictionary groups' ~100 KB tables need one 1024-thread workgroup
                 const bool one_wg = e->sg_lds[q] > SCAN_LDS_TWO_WG;
                 const int nt = one_wg ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
-                (!wb ? k_scan<true>
-                     : q == 0 ? k_scan<true, SCAN_BLOCK, true>
-                     : one_wg ? k_scan<false, SCAN_BLOCK_WIDE, true> : k_scan<false, SCAN_BLOCK, true>)<<<
+                (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
                     (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], st>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
                 if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
@@ -5346,11 +5309,9 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     if (max_lds > 64 * 1024 &&
         (hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
-         hipFuncSetAttribute((const void*)k_scan<true, SCAN_BLOCK, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)max_lds) != hipSuccess ||
-         hipFuncSetAttribute((const void*)k_scan<false, SCAN_BLOCK, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)max_lds) != hipSuccess ||
-         hipFuncSetAttribute((const void*)k_scan<false, SCAN_BLOCK_WIDE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+         hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan<false, SCAN_BLOCK_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)max_lds) != hipSuccess ||
          hipFuncSetAttribute((const void*)k_halo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) != hipSuccess))
         return fail("cannot raise LDS limit");
