@@ -151,7 +151,9 @@ int pii_reserve(struct pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint
  * pii_context_resize allocate outside it), e.g. on a GPU shared with other work; 0 = no limit.  A call that
  * would need more fails with PII_E_NOMEM and commits nothing (the service maps it to
  * "[DLP_PROCESSING_ERROR] {transcript}", main.py:770-773); buffers already held stay valid.
- * pii_scratch_bytes reports what the work buffers hold now. */
+ * pii_scratch_bytes reports what the work buffers hold now.  A growing buffer is allocated before the
+ * old one is freed (a failed growth leaves the engine usable), so growing one of the large arenas
+ * needs its old and new size at once for a moment; pii_reserve up front avoids growth in the loop. */
 int pii_set_scratch_limit(struct pii_engine* e, uint64_t bytes);
 int pii_scratch_bytes(struct pii_engine* e, uint64_t* used);
 /* wait for the last device call; totals[0] = output bytes, [1] = spans, [2] = error flags */
