@@ -92,6 +92,35 @@ def test_relaxed_scan_is_superset_of_true_starts(compiled, sim):
                     assert pid in reported.get(s, set()), (compiled.rules.patterns[pid].type_name, t, s)
 
 
+def test_digit_run_prefixes_stay_supersets(compiled, sim):
+    """The exact digit-run prefixes (passport 8-9 digits, 10-digit phone / DOD id: the SCAN automaton
+    counts the run and checks its closing boundary) still report every true start: runs of 1-20 digits
+    with letter / separator neighbours, where an off-by-one in the count would drop a match."""
+    r = random.Random(11)
+    pats = [re.compile(p.pattern.encode()) for p in compiled.rules.patterns]
+    names = {"US_PASSPORT", "PHONE_NUMBER", "DOD_ID_NUMBER"}
+    pids = [i for i, p in enumerate(compiled.rules.patterns) if p.type_name in names]
+    assert pids
+    for _ in range(600):
+        parts = []
+        for _ in range(r.randrange(1, 4)):
+            parts.append(r.choice([b"", b"A", b"x", b" ", b"-", b"(", b"Z"]))
+            parts.append(bytes(r.choice(b"0123456789") for _ in range(r.randrange(1, 21))))
+            parts.append(r.choice([b"", b" ", b".", b"a", b"_", b"-"]))
+        t = b"".join(parts)
+        ev = sim.scan(t, True)
+        reported = {}
+        for pos, sd, sk in ev:
+            cd, _ = sim._classes(t, pos)
+            a = int(sim.dacc[sd, cd])
+            reported[pos] = {int(sim.d_ids[i]) for i in range(int(sim.d_off[a]), int(sim.d_off[a + 1]))}
+        for pid in pids:
+            for s in range(len(t)):
+                m = pats[pid].match(t, s)
+                if m and m.end() > s:
+                    assert pid in reported.get(s, set()), (compiled.rules.patterns[pid].type_name, t, s)
+
+
 def test_blob_roundtrip(C, compiled):
     back = C.blob_sections(compiled.blob)
     assert list(back) == list(compiled.sections)
