@@ -2400,35 +2400,49 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
     // the row's chain starts are compacted first, so the chains run side by side (a thread per lane
     // left most threads idle and ran the few chains of a row one slice of 256 lanes after another)
     constexpr uint32_t FIX_CAP = 256;
+    static_assert(FIX_CAP >= 256, "a slice of the launch's 256 lanes always fits an emptied list");
     __shared__ uint32_t s_chain[FIX_CAP];
-    __shared__ uint32_t s_nc;
+    __shared__ uint32_t s_wc[4];
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     SelTabs Tb = sel_tabs(lb, li);
     if (io.g_xoff) {
         Tb.xoff = io.g_xoff;
         Tb.xids = io.g_xids;
     }
-    auto run = [&](uint32_t j) {
-        uint32_t c = j + 1;
-        while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
-        select_run<EXT>(R, Tb, g, io, j, c);
-    };
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (uint32_t ri = blockIdx.x; ri < *long_count; ri += gridDim.x) {
         uint32_t ca, kb;
         int64_t s_r, e_r;
         row_lanes(g, long_rows[ri], ca, kb, s_r, e_r);
-        __syncthreads();
-        if (threadIdx.x == 0) s_nc = 0;
-        __syncthreads();
-        for (uint32_t j = ca + threadIdx.x; j < kb; j += blockDim.x) {
-            if (dirty[j] || !dirty[j + 1]) continue;
-            const uint32_t at = atomicAdd(&s_nc, 1u);
-            if (at < FIX_CAP) s_chain[at] = j;
-            else run(j);
+        // chain starts listed in lane order one slice of 256 lanes at a time; the listed chains run
+        // when the next slice might not fit and after the last one -- ONE call site of select_run, so
+        // it is inlined (two sites kept it a call: 180 VGPRs and 560 B of scratch per lane)
+        uint32_t n = 0;                                   // chains listed (block-uniform)
+        for (uint32_t j0 = ca;; j0 += 256) {
+            const bool done = j0 >= kb;
+            const uint32_t j = j0 + threadIdx.x;
+            const bool st = !done && j < kb && !dirty[j] && dirty[j + 1];
+            const uint32_t tot = (uint32_t)__syncthreads_count(st);
+            if (done || n + tot > FIX_CAP) {
+                for (uint32_t k = threadIdx.x; k < n; k += 256) {
+                    const uint32_t j1 = s_chain[k];
+                    uint32_t c = j1 + 1;
+                    while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
+                    select_run<EXT>(R, Tb, g, io, j1, c);
+                }
+                n = 0;
+                __syncthreads();                          // the list is free again
+            }
+            if (done) break;
+            const uint64_t bal = __ballot(st);
+            if (lane == 0) s_wc[wv] = (uint32_t)__popcll(bal);
+            __syncthreads();
+            uint32_t pre = n;
+            for (int w = 0; w < wv; ++w) pre += s_wc[w];
+            if (st) s_chain[pre + __popcll(bal & ((1ull << lane) - 1))] = j;
+            n += tot;
+            __syncthreads();                              // (s_wc is reused by the next slice)
         }
-        __syncthreads();
-        const uint32_t n = min(s_nc, FIX_CAP);
-        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) run(s_chain[k]);
     }
 }
 
