@@ -31,8 +31,9 @@ def reduce_histogram(hist: np.ndarray, group=None) -> np.ndarray:
     """Sum per-infoType counts over all ranks (int64; the last slot may carry the span total)."""
     import torch
     import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_available() or not dist.is_initialized():
         return hist.astype(np.int64)
+    # (world size 1 still issues the collective: the same RCCL code path as N ranks, tests/test_rccl_gpu.py)
     backend = dist.get_backend(group)
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     t = torch.from_numpy(np.ascontiguousarray(hist, dtype=np.int64)).to(dev)

@@ -46,6 +46,7 @@ re-scan the README describes; ``conversation_ended`` drops a conversation's wind
 """
 from __future__ import annotations
 
+import logging
 import threading
 import time
 from collections import OrderedDict
@@ -101,17 +102,25 @@ class SlotMap:
     window history (the aggregator keeps a conversation's utterances until it ends).  Among those,
     the least recently used conversation that is not pinned (part of the batch being built) goes
     first; its slot is cleared (``on_evict``).  When no slot can be reused the table GROWS
-    (``on_grow(n)``, pii_context_resize: live records are kept), so a live context is never dropped."""
+    (``on_grow(n)``, pii_context_resize: live records are kept), so a live context is never dropped.
 
-    SCAN = 64            # LRU entries examined for a reusable slot before the table grows instead
+    The victim search walks the whole LRU order (the table grows only when NO slot is reusable); the
+    live entries it passes over move to the most-recently-used end, so the next search starts at
+    entries it has not just examined and a block of long-lived (e.g. windowed, never ended)
+    conversations at the LRU end costs one pass, not one per call.  (A search runs only when the
+    free list is empty, and a failed one doubles it, so the cost per slot handed out stays O(1)
+    amortised.)  When the table cannot grow -- the device has no memory for the doubled table
+    (``on_grow`` raises PiiError NOMEM) or ``max_slots`` is reached -- the PiiError goes to the
+    caller, which answers that conversation's rows with the reference's error string."""
 
     def __init__(self, n_slots: int, on_evict: Optional[Callable[[int], None]] = None,
-                 on_grow: Optional[Callable[[int], None]] = None):
+                 on_grow: Optional[Callable[[int], None]] = None, max_slots: Optional[int] = None):
         if n_slots < 3:
             raise ValueError("need at least 3 slots (slot 0 is reserved)")
         self.n_slots = n_slots
         self.on_evict = on_evict
         self.on_grow = on_grow
+        self.max_slots = max_slots
         self._map: "OrderedDict[object, int]" = OrderedDict()
         self._free = list(range(n_slots - 1, 0, -1))
         self.live_until: Dict[int, int] = {}      # slot -> time its context record expires (us)
@@ -141,40 +150,68 @@ class SlotMap:
         self.live_until.pop(slot, None)
         self.windowed.discard(slot)
 
+    def _victim(self, pinned: Optional[set], now_us: Optional[int]):
+        """the least recently used reusable unpinned conversation, or None; the live entries passed
+        over move to the MRU end"""
+        victim, passed = None, []
+        for c, cs in self._map.items():
+            if pinned and c in pinned:
+                continue
+            if self.reusable(cs, now_us):
+                victim = c
+                break
+            passed.append(c)
+        for c in passed:
+            self._map.move_to_end(c)
+        return victim
+
     def get(self, conversation_id, pinned: Optional[set] = None, now_us: Optional[int] = None) -> int:
         s = self._map.get(conversation_id)
         if s is not None:
             self._map.move_to_end(conversation_id)
             return s
         if not self._free:
-            victim, seen = None, 0
-            for c, cs in self._map.items():
-                if pinned and c in pinned:
-                    continue
-                if self.reusable(cs, now_us):
-                    victim = c
-                    break
-                seen += 1
-                if seen >= self.SCAN:
-                    break
-            if victim is not None:
+            victim = self._victim(pinned, now_us)
+            if victim is None:
+                self._grow()
+            else:
                 s = self._map.pop(victim)
                 self._forget(s)
                 if self.on_evict:
                     self.on_evict(s)
                 self._map[conversation_id] = s
                 return s
-            self._grow()
         s = self._free.pop()
         self._map[conversation_id] = s
         return s
 
     def _grow(self) -> None:
         n = self.n_slots * 2
+        if self.max_slots is not None and n > self.max_slots:
+            raise PiiError(PII_E_NOMEM, f"conversation table at its maximum of {self.max_slots} slots")
         if self.on_grow:
-            self.on_grow(n)                       # raises if the device cannot hold the larger table
+            self.on_grow(n)                       # raises PiiError if the device cannot hold the larger table
         self._free = list(range(n - 1, self.n_slots - 1, -1)) + self._free
         self.n_slots = n
+
+    def assign(self, conversation_ids: Sequence, pinned: Optional[set], now_us: Optional[int]
+               ) -> Tuple[List[Optional[int]], int]:
+        """slots for a run of rows: None for the rows of a conversation that got no slot (the table
+        could neither reuse a slot nor grow), with the PiiError code of that failure (0: none)"""
+        out: List[Optional[int]] = []
+        failed: Dict[object, int] = {}
+        code = 0
+        for cid in conversation_ids:
+            if cid in failed:
+                out.append(None)
+                continue
+            try:
+                out.append(self.get(cid, pinned, now_us))
+            except PiiError as e:
+                failed[cid] = e.code
+                code = e.code
+                out.append(None)
+        return out, code
 
     def peek(self, conversation_id) -> Optional[int]:
         return self._map.get(conversation_id)
@@ -208,7 +245,7 @@ class PiiService:
 
     def __init__(self, engine: Optional[Engine] = None, n_slots: int = 1 << 16,
                  ttl_seconds: int = CONTEXT_TTL_SECONDS, clock: Callable[[], float] = time.time, device: int = 0,
-                 time_base: str = "wall", ner=None, ner_max_len: int = 64):
+                 time_base: str = "wall", ner=None, ner_max_len: int = 64, max_slots: Optional[int] = None):
         if time_base not in ("wall", "payload"):
             raise ValueError("time_base must be 'wall' or 'payload'")
         self.engine = engine if engine is not None else Engine.from_rules(device=device, n_conv_slots=n_slots,
@@ -218,7 +255,8 @@ class PiiService:
         self.time_base = time_base
         self._payload_now: Optional[int] = None
         self.lock = threading.Lock()
-        self.slots = SlotMap(self.engine.n_slots, on_evict=self._evict, on_grow=self.engine.context_resize)
+        self.slots = SlotMap(self.engine.n_slots, on_evict=self._evict, on_grow=self.engine.context_resize,
+                             max_slots=max_slots)
         self.group_of_type: Dict[str, int] = {}
         for g, t in enumerate(self.engine.group_types):
             self.group_of_type.setdefault(t, g)
@@ -305,6 +343,31 @@ class PiiService:
         h = n // 2
         return np.concatenate([self._context_fallback(texts[:h], slots[:h], roles[:h], ts[:h]),
                                self._context_fallback(texts[h:], slots[h:], roles[h:], ts[h:])])
+
+    def _without_slots(self, part, slots, code, texts, ts, call, window=False) -> List[str]:
+        """A run some of whose conversations got no slot (SlotMap.assign): those rows get the
+        reference's error string and store nothing; the other rows run as usual (dropping whole
+        conversations keeps the batch contract).  Called with the service lock held."""
+        keep = [k for k, sl in enumerate(slots) if sl is not None]
+        red: Dict[int, str] = {k: error_string(code, part[k]["text"]) for k in range(len(part)) if slots[k] is None}
+        if keep:
+            k_texts = [texts[k] for k in keep]
+            k_slots = [slots[k] for k in keep]
+            k_roles = [role_code(part[k].get("participant_role")) for k in keep]
+            k_ts = [ts[k] for k in keep]
+            try:
+                res = call(k_texts, k_slots, k_roles, k_ts)
+            except PiiError as e:
+                self._note(k_slots, k_roles, [part[k]["text"] for k in keep], k_ts,
+                           self._context_fallback(k_texts, k_slots, k_roles, k_ts))
+                red.update({k: error_string(e.code, part[k]["text"]) for k in keep})
+            else:
+                if window:
+                    for sl in k_slots:
+                        self.slots.note_window(sl)
+                self._note(k_slots, k_roles, [part[k]["text"] for k in keep], k_ts, res.ctx_info)
+                red.update({k: _dec(res.text(j)) for j, k in enumerate(keep)})
+        return [red[k] for k in range(len(part))]
 
     # ---------------------------------------------------------------- reference seam (main.py:580)
     def call_dlp_for_redaction(self, transcript: str, context: Optional[dict]) -> str:
@@ -433,8 +496,17 @@ class PiiService:
                     else:
                         rows.append((slot, i, utt, ROLE_CUSTOMER, False))
                 else:
-                    slot = self.slots.get(cid, pinned, now)
+                    try:
+                        slot = self.slots.get(cid, pinned, now)
+                    except PiiError as e:
+                        # no slot for the conversation (the table could neither reuse one nor grow):
+                        # the request is answered as after a failed DLP call, nothing is stored
+                        key = "context_stored" if kind == "agent" else "context_used"
+                        out[i] = ({"redacted_transcript": error_string(e.code, data["transcript"]), key: False}, 200)
+                        continue
                     rows.append((slot, i, data["transcript"], ROLE_AGENT if kind == "agent" else ROLE_CUSTOMER, False))
+            if not rows:
+                return
             # the batch contract: a slot's rows contiguous, in arrival order
             first: Dict[int, int] = {}
             for k, r in enumerate(rows):
@@ -470,20 +542,30 @@ class PiiService:
                         lines = red.splitlines() if split_last else [red]
                         out[i] = ({"redacted_utterance": lines[-1] if lines else ""}, 200)
                 return
-            self._note(slots, roles, [r[2] for r in rows], ts, res.ctx_info)
+            # The engine call has committed (context stored on the device): from here on every request
+            # of the call is answered, so a caller never re-runs it (a re-run would store its context
+            # twice).  A failure while building a response is that request's own 500, as an exception
+            # raised after the SETEX in the reference's handler would be.
+            try:
+                self._note(slots, roles, [r[2] for r in rows], ts, res.ctx_info)
+            except Exception:                           # noqa: BLE001 - the call stays answered
+                logging.getLogger(__name__).exception("host context bookkeeping failed after a committed call")
             for k, (slot, i, text, role, split_last) in enumerate(rows):
                 kind, data = reqs[i]
-                red = _dec(res.text(k))
-                g = int(res.ctx_info[k])
-                if kind == "agent":
-                    out[i] = ({"redacted_transcript": red, "context_stored": g >= 0}, 200)
-                elif kind == "customer":
-                    out[i] = ({"redacted_transcript": red, "context_used": g >= 0}, 200)
-                else:
-                    if split_last:
-                        lines = red.splitlines()
-                        red = lines[-1] if lines else ""
-                    out[i] = ({"redacted_utterance": red}, 200)
+                try:
+                    red = _dec(res.text(k))
+                    g = int(res.ctx_info[k])
+                    if kind == "agent":
+                        out[i] = ({"redacted_transcript": red, "context_stored": g >= 0}, 200)
+                    elif kind == "customer":
+                        out[i] = ({"redacted_transcript": red, "context_used": g >= 0}, 200)
+                    else:
+                        if split_last:
+                            lines = red.splitlines()
+                            red = lines[-1] if lines else ""
+                        out[i] = ({"redacted_utterance": red}, 200)
+                except Exception:                       # noqa: BLE001 - answered, never re-run
+                    out[i] = ({"error": "Internal Server Error"}, 500)
 
     # ---------------------------------------------------------------- aggregator re-scan (a12)
     def rescan_window_batch(self, rows: Sequence[dict], window_n: int = 5, slot_bytes: int = 8192) -> List[str]:
@@ -504,7 +586,11 @@ class PiiService:
                 texts = [_enc(r["text"]) for r in part]
                 ts = [self._row_ts(r, now) for r in part]
                 now = self._now_us()
-                slots = [self.slots.get(r["conversation_id"], pinned, now) for r in part]
+                slots, code = self.slots.assign([r["conversation_id"] for r in part], pinned, now)
+                if code:
+                    out.extend(self._without_slots(part, slots, code, texts, ts, self.engine.rescan_window,
+                                                   window=True))
+                    continue
                 roles = [role_code(r.get("participant_role")) for r in part]
                 try:
                     res = self.engine.rescan_window(texts, slots, roles, ts)
@@ -544,7 +630,10 @@ class PiiService:
                 texts = [_enc(r["text"]) for r in part]
                 ts = [self._row_ts(r, now) for r in part]
                 now = self._now_us()
-                slots = [self.slots.get(r["conversation_id"], pinned, now) for r in part]
+                slots, code = self.slots.assign([r["conversation_id"] for r in part], pinned, now)
+                if code:
+                    out.extend(self._without_slots(part, slots, code, texts, ts, self._run))
+                    continue
                 roles = [role_code(r.get("participant_role")) for r in part]
                 try:
                     res = self._run(texts, slots, roles, ts)

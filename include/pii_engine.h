@@ -166,7 +166,12 @@ int pii_context_set(struct pii_engine* e, uint32_t slot, int32_t group, int64_t 
  * keeps every context:{id} key until its TTL runs out (main.py:163, 366-374), so the host slot map
  * grows the table instead of evicting a conversation whose record is still live.  Records and
  * window histories of the existing slots are kept; new slots start empty.  Synchronous.  On failure
- * (PII_E_NOMEM) the table is unchanged. */
+ * (PII_E_NOMEM) the table is unchanged.  Peak device memory: the new tables are allocated and filled
+ * before the old ones are freed, so the call briefly holds old + new = (n_old + n_conv_slots) x
+ * (16 B of context record + with the window enabled, window_n x 16 B of ring entries + 8 B of ring
+ * counters + slot_bytes of ring text) -- e.g. doubling 64k slots with N = 5 and 8 KiB rings holds
+ * about 1.6 GB at once.  The service answers a failed growth with the reference's error string
+ * for that conversation (service.SlotMap, "[DLP_PROCESSING_ERROR] {transcript}"). */
 int pii_context_resize(struct pii_engine* e, uint32_t n_conv_slots);
 /* The context half of pii_scan_redact alone, for rows whose redaction failed: the reference stores
  * an agent utterance's context even when its DLP call failed (call_dlp_for_redaction never raises;
