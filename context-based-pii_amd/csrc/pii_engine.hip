@@ -2020,43 +2020,71 @@ __device__ __forceinline__ SelTabs sel_tabs(const uint8_t* lb, const LdsImage& l
     return T;
 }
 
-// select over the pairs of lanes c0..c1 as ONE sequential pass (the state carries across the lanes).
-// EXT: the lanes' external candidates (SelIO::ext) are merged into the pair stream in (row, start)
-// order; they take part in overlap resolution (A.6) and min_likelihood like any finding, but not in
-// finditer skipping (they have no pattern) nor as excluders.
-template <bool EXT>
-__device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t c0,
-                           uint32_t c1) {
-    const int T = R.T;
-    uint2* __restrict__ spill = io.spill + io.lane_pair[c0];
+// The selection state machine of ONE pass over candidates in (row, start, accept-set) order: finditer
+// skipping per pattern, exclusion (A.5), best-per-start and greedy overlap resolution (A.6), output
+// sizing.  Findings go to the current LANE's arena (fd + fd_base), in (utterance, start) order.  Fed
+// by select_run (k_select / k_sel_fix: candidates from the global pair queue).
+struct LaneSel {
     // per-utterance state
-    uint32_t u = 0xffffffffu;
-    int v = 0, minlik = 0;
+    uint32_t u;
+    int v, minlik;
     int lp[LIVE], le[LIVE];
-    uint32_t n_spill = 0;
-    bool spilled = false;
+    uint32_t n_spill;
+    bool spilled;
     int ex_s[NE_MAX], ex_e[NE_MAX], ex_t[NE_MAX];
-    uint32_t ex_valid = 0;
-    int max_end = 0;
-    uint32_t nf_u = 0;
-    int delta_u = 0;
+    uint32_t ex_valid;
+    int max_end;
+    uint32_t nf_u;
+    int delta_u;
     // per-lane state
-    Lane Lg{};
-    uint32_t lane = c0;
-    pii_span* fdl = nullptr;
-    uint32_t nfl = 0;
-    int rdx = 0, rdy = 0;
-    uint32_t reach = 0;
+    Lane Lg;
+    pii_span* fdl;
+    uint32_t nfl;
+    int rdx, rdy;
+    uint32_t reach;
     // per-start state
-    int s = -1, best_e = -1, best_t = 0, best_lik = 0;
+    int s, best_e, best_t, best_lik;
+    uint2* spill;           // the lane run's list of (pattern, end) once more than LIVE patterns are live
+
+    __device__ __forceinline__ void init(uint2* sp) {
+        spill = sp;
+        u = 0xffffffffu;
+        v = 0;
+        minlik = 0;
+        n_spill = 0;
+        spilled = false;
+        ex_valid = 0;
+        max_end = 0;
+        nf_u = 0;
+        delta_u = 0;
+        Lg = Lane{};
+        fdl = nullptr;
+        nfl = 0;
+        rdx = rdy = 0;
+        reach = 0;
+        s = -1;
+        best_e = -1;
+        best_t = 0;
+        best_lik = 0;
 #pragma unroll
-    for (int q = 0; q < LIVE; ++q) {
-        lp[q] = -1;
-        le[q] = -1;
+        for (int q = 0; q < LIVE; ++q) {
+            lp[q] = -1;
+            le[q] = -1;
+        }
+#pragma unroll
+        for (int x = 0; x < NE_MAX; ++x) ex_s[x] = ex_e[x] = ex_t[x] = 0;
     }
-    auto cut_lo_row = [&](uint32_t x) { return Lg.clo && x == Lg.u0; };
-    auto cut_row = [&](uint32_t x) { return cut_lo_row(x) || (Lg.chi && x == Lg.u1 - 1); };
-    auto flush_start = [&]() {
+    __device__ __forceinline__ bool cut_lo_row(uint32_t x) const { return Lg.clo && x == Lg.u0; }
+    __device__ __forceinline__ bool cut_row(uint32_t x) const { return cut_lo_row(x) || (Lg.chi && x == Lg.u1 - 1); }
+    // a new lane of the pass: its findings arena and per-lane outputs start empty
+    __device__ __forceinline__ void begin_lane(const Geo& g, const SelIO& io, const RulesDev& R, uint32_t lane) {
+        Lg = g_lane(g, lane);
+        fdl = io.fd + fd_base(Lg, lane, R.min_len);
+        nfl = 0;
+        rdx = rdy = 0;
+        reach = 0;
+    }
+    __device__ __forceinline__ void flush_start(const SelTabs& Tb) {
         if (best_e >= 0 && s >= max_end) {
             pii_span f;
             f.utt = u;
@@ -2077,20 +2105,21 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             nf_u += cut_r ? 0u : 1u;
         }
         best_e = -1;
-    };
+    }
     // a whole row's output length, written (not added: k_sel_fix re-runs whole lanes, and a re-run
     // must not count the whole rows of its lanes twice); rows without findings keep the length
     // k_chunk_index wrote
-    auto flush_utt = [&]() {
+    __device__ __forceinline__ void flush_utt(const Geo& g, const SelIO& io) {
         if (nf_u) io.out_len[u] = (uint32_t)(g_off(g, u + 1) - g_off(g, u)) + (uint32_t)delta_u;
-    };
+    }
     // candidate (row pu, start ps, end e) enters: row / start transitions
-    // pv: the row's context variant (from its SelRec), or -1: derive it from role / ctx
-    auto enter = [&](uint32_t pu, int ps, int e, int pv) {
+    // pv: the row's context variant, or -1: derive it from role / ctx
+    __device__ __forceinline__ void enter(const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t pu, int ps, int e,
+                                          int pv) {
         if (pu != u) {
             if (u != 0xffffffffu) {
-                flush_start();
-                flush_utt();
+                flush_start(Tb);
+                flush_utt(g, io);
             }
             u = pu;
             v = pv >= 0 ? pv : (io.role[u] == PII_ROLE_CUSTOMER && io.ctx[u] >= 0) ? io.ctx[u] + 1 : 0;
@@ -2108,13 +2137,13 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             delta_u = 0;
             s = ps;
         } else if (ps != s) {
-            flush_start();
+            flush_start(Tb);
             s = ps;
         }
         if (Lg.chi && u == Lg.u1 - 1) reach = max(reach, (uint32_t)e);
-    };
+    }
     // a valid candidate of type t (excluder slot xi, 0xff: none) competes for its start
-    auto consider = [&](int t, int lik, int e, int xi) {
+    __device__ __forceinline__ void consider(const SelTabs& Tb, int T, int t, int lik, int e, int xi) {
         const uint32_t x0 = Tb.xoff[v * T + t], x1 = Tb.xoff[v * T + t + 1];
         bool excluded = false;
         for (uint32_t q = x0; q < x1; ++q) {
@@ -2132,10 +2161,11 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             best_t = t;
             best_lik = lik;
         }
-    };
-    auto pair = [&](const SelRec& P, int e) {
-        enter(P.u, P.ps, e, (int)(P.p >> 16));
-        const int p = (int)(P.p & 0xffffu);
+    }
+    // a matched pair: row pu, start ps (row relative), pattern p, context variant pv, end e, likelihood lik
+    __device__ __forceinline__ void pair(const SelTabs& Tb, const Geo& g, const SelIO& io, int T, uint32_t pu, int ps,
+                                         int p, int pv, int e, int lik) {
+        enter(Tb, g, io, pu, ps, e, pv);
         const int t = Tb.dtype[p];
         if (!Tb.ven[v * T + t]) return;
         int prev_end = -1;
@@ -2180,7 +2210,6 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
             }
         }
         const int xi = Tb.dex[p];
-        const int lik = P.lik;
         if (lik < minlik) {                        // invalid (-1) or below min_likelihood
             if (xi != 0xff) ex_valid &= ~(1u << xi);
             return;
@@ -2195,8 +2224,34 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 }
             ex_valid |= 1u << xi;
         }
-        consider(t, lik, e, xi);
-    };
+        consider(Tb, T, t, lik, e, xi);
+    }
+    // the end of the lane: the pending start and (unless the row continues into the next lane) the
+    // utterance end; the lane's outputs
+    __device__ __forceinline__ void end_lane(const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t lane) {
+        if (u != 0xffffffffu) {
+            flush_start(Tb);
+            if (!(Lg.chi && u == Lg.u1 - 1)) {
+                flush_utt(g, io);
+                u = 0xffffffffu;
+            }
+        }
+        io.lane_nf[lane] = nfl;
+        io.lane_rd[lane] = make_int2(rdx, rdy);
+        if (Lg.chi) io.lane_reach[lane] = reach;
+    }
+};
+
+// select over the pairs of lanes c0..c1 as ONE sequential pass (the state carries across the lanes).
+// EXT: the lanes' external candidates (SelIO::ext) are merged into the pair stream in (row, start)
+// order; they take part in overlap resolution (A.6) and min_likelihood like any finding, but not in
+// finditer skipping (they have no pattern) nor as excluders.
+template <bool EXT>
+__device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t c0,
+                           uint32_t c1) {
+    const int T = R.T;
+    LaneSel S;
+    S.init(io.spill + io.lane_pair[c0]);
     // external candidates: cursor over the lane's rows [u0, u1); a cut row contributes the spans
     // whose start lies in the lane's byte range.  Every span is checked (start < end <= row length,
     // sorted by start, type < T, likelihood 1..5); a bad one sets ERR_EXT and is skipped.
@@ -2208,7 +2263,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
         xk = 0;
         xprev = 0;
         xn = 0;
-        if (r < Lg.u1) {
+        if (r < S.Lg.u1) {
             xn = io.ext_n[r];
             if (xn > io.ext_stride) {
                 atomicOr(io.err, ERR_EXT);
@@ -2218,7 +2273,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     };
     auto xload = [&]() {
         xhave = false;
-        while (xu < Lg.u1) {
+        while (xu < S.Lg.u1) {
             if (xk < xn) {
                 X = io.ext[(uint64_t)xu * io.ext_stride + xk++];
                 const int64_t r0 = g_off(g, xu), rl = g_off(g, xu + 1) - r0;
@@ -2229,8 +2284,8 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 }
                 xprev = X.start;
                 const int64_t a = r0 + X.start;
-                if (Lg.clo && xu == Lg.u0 && a < (int64_t)Lg.lo) continue;
-                if (Lg.chi && xu == Lg.u1 - 1 && a >= (int64_t)Lg.hi) {
+                if (S.Lg.clo && xu == S.Lg.u0 && a < (int64_t)S.Lg.lo) continue;
+                if (S.Lg.chi && xu == S.Lg.u1 - 1 && a >= (int64_t)S.Lg.hi) {
                     xk = xn;
                     continue;
                 }
@@ -2243,18 +2298,14 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     };
     auto ext_cand = [&]() {
         const int e = (int)X.end, t = X.info_type, lik = X.likelihood;
-        enter(X.utt, (int)X.start, e, -1);
-        if (Tb.ven[v * T + t] && lik >= minlik) consider(t, lik, e, 0xff);
+        S.enter(Tb, g, io, X.utt, (int)X.start, e, -1);
+        if (Tb.ven[S.v * T + t] && lik >= S.minlik) S.consider(Tb, T, t, lik, e, 0xff);
         xload();
     };
-    for (lane = c0; lane <= c1; ++lane) {
-        Lg = g_lane(g, lane);
-        fdl = io.fd + fd_base(Lg, lane, R.min_len);
-        nfl = 0;
-        rdx = rdy = 0;
-        reach = 0;
+    for (uint32_t lane = c0; lane <= c1; ++lane) {
+        S.begin_lane(g, io, R, lane);
         if (EXT) {
-            xrow(Lg.u0);
+            xrow(S.Lg.u0);
             xload();
         }
         const uint32_t np = io.lane_np[lane];
@@ -2302,22 +2353,12 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 if (ok) r1 = io.sel[pbase + i1];
                 if (EXT)
                     while (xhave && (X.utt < r.u || (X.utt == r.u && (int)X.start <= r.ps))) ext_cand();
-                pair(r, e);
+                S.pair(Tb, g, io, T, r.u, r.ps, (int)(r.p & 0xffffu), (int)(r.p >> 16), e, r.lik);
             }
         }
         if (EXT)
             while (xhave) ext_cand();
-        // the pending start and (unless the row continues into the next lane) the utterance end here
-        if (u != 0xffffffffu) {
-            flush_start();
-            if (!(Lg.chi && u == Lg.u1 - 1)) {
-                flush_utt();
-                u = 0xffffffffu;
-            }
-        }
-        io.lane_nf[lane] = nfl;
-        io.lane_rd[lane] = make_int2(rdx, rdy);
-        if (Lg.chi) io.lane_reach[lane] = reach;
+        S.end_lane(Tb, g, io, lane);
     }
 }
 
