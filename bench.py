@@ -1178,7 +1178,9 @@ def window_main(args):
                                                                if c5path else ""),
                    "rules": args.window_rules, "mode": eng.window_mode(),
                    "rows_per_step": C, "parallelism": "conversation-sharded x1",
-                   "bytes_per_gpu": int(meta.offsets[-1])},
+                   # a step processes one new utterance per conversation: its bytes are the per-step
+                   # workload; the whole U-step stream stays resident in HBM beside it
+                   "bytes_per_gpu": int(new_b / K), "resident_stream_bytes": int(meta.offsets[-1])},
         "windows_per_s": round(K * C / elapsed, 1),
         "window_output_MBps": round(out_b / elapsed / 1e6, 1),
         "naive_equivalent_bytes_rescanned_per_step": int(win_in / K),

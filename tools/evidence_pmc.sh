@@ -16,6 +16,12 @@ for W in scan config5 window long; do
   bash tools/pmc_traffic.sh "gpurun_out/$TAG/traffic_$W" "$W" --steps 2 --warmup 1 --no-cpu-baseline > "$O/traffic_$W.log" 2>&1 || { echo "PMC $W FAILED"; tail -5 "$O/traffic_$W.log"; exit 1; }
   echo "PMC $W ok"
 done
+# bound / occupancy passes (wave-cycle split, achieved waves per SIMD) of every k_scan instantiation:
+# config 2 (group 0), config 5 (narrow and WIDE groups), the window step
+for W in scan config5 window; do
+  bash tools/pmc_bound.sh "gpurun_out/$TAG/bound_$W" --workload "$W" --steps 2 --warmup 1 --no-cpu-baseline > "$O/bound_$W.log" 2>&1 || { echo "BOUND $W FAILED"; tail -5 "$O/bound_$W.log"; exit 1; }
+  echo "BOUND $W ok"
+done
 cd /tmp && export TMPDIR=/tmp
 for W in scan config5 window; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$W" -o run -- python "$R/bench.py" --workload "$W" --steps 10 --warmup 3 --no-cpu-baseline > "$O/prof_$W.log" 2>&1 || { echo "PROF $W FAILED"; exit 1; }

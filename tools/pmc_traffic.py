@@ -80,17 +80,26 @@ def algorithmic_bytes(kernel, b):
     return None
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, tail=None):
+    """counter value per dispatch, per kernel (dispatch order); tail = (steps, total steps): keep only
+    the dispatches of the last `steps` of `total` bench steps (the timed, steady-state ones: a window
+    re-scan's first N steps fill the windows)"""
     acc = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
-            acc[(k, r.get("Dispatch_Id", len(acc)))].append(float(r["Counter_Value"]))
+            acc[(k, int(r.get("Dispatch_Id", len(acc))))].append(float(r["Counter_Value"]))
     out = defaultdict(list)
-    for (k, _), v in acc.items():
+    for (k, _), v in sorted(acc.items(), key=lambda kv: kv[0][1]):
         out[k].append(sum(v))          # sum over the counter's instances of one dispatch
+    if tail:
+        steps, total = tail
+        for k in out:
+            n = len(out[k])
+            if n >= total and n % total == 0:            # the kernel runs n / total times per step
+                out[k] = out[k][n - n // total * steps:]
     return out
 
 
@@ -115,15 +124,21 @@ def lds_unit(d):
 def main():
     d = sys.argv[1]
     w = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "scan"
-    fetch = per_kernel(os.path.join(d, "fetch"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(d, "write"), "WRITE_SIZE")
+    bench = [json.loads(l) for l in open(os.path.join(d, "fetch.log")) if l.startswith("{")]
+    tail = None
+    if bench and w.startswith("window"):
+        # only the timed steps: the bench's warm-up fills the windows (warmup >= N)
+        K, W0 = int(bench[-1]["steps"]), int(bench[-1]["warmup"])
+        tail = (K, K + W0)
+    fetch = per_kernel(os.path.join(d, "fetch"), "FETCH_SIZE", tail)
+    write = per_kernel(os.path.join(d, "write"), "WRITE_SIZE", tail)
     calib = per_kernel(os.path.join(d, "calib"), "FETCH_SIZE")
     # every lane_read launch reads CALIB_BYTES (k_lane_rev at 512/1024/2048 B per lane, the streams)
     corrs = {pat: (CALIB_BYTES / (mean(calib[k]) * 1024) if calib.get(k) else None)
              for pat, k in CALIB_KERNELS.items()}
     corr = corrs["lane_rev"]
-    bench = [json.loads(l) for l in open(os.path.join(d, "fetch.log")) if l.startswith("{")]
-    n_bytes = bench[-1]["config"].get("bytes_per_gpu", bench[-1]["config"].get("bytes_per_step")) if bench else None
+    cfg = bench[-1]["config"] if bench else {}
+    n_bytes = cfg.get("resident_stream_bytes", cfg.get("bytes_per_gpu", cfg.get("bytes_per_step"))) if bench else None
     h = hashlib.sha256()
     for f in SOURCES:
         h.update(open(os.path.join(ROOT, f), "rb").read())
