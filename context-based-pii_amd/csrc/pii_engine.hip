@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -1889,7 +1890,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
                                                           const int32_t* __restrict__ pend,
                                                           const PairRes* __restrict__ pres, SelRec* __restrict__ sel,
                                                           const uint32_t* __restrict__ g_roff,
-                                                          const uint16_t* __restrict__ g_rids) {
+                                                          const uint16_t* __restrict__ g_rids, uint32_t split) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     EvalTabs E = eval_tabs(lb, li);
@@ -1900,7 +1901,11 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint8_t* text = text0 + offs[0];
     __shared__ uint32_t s_mp[PAIR_WAVES + 1];
     const uint64_t seg = pair_segment(min((uint64_t)*pair_count, pair_cap), nseg * PAIR_WAVES);
-    for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
+    // work unit gj = part (gj % split) of k_pair_first workgroup gj / split's matched pairs: with split
+    // > 1 the grid runs several rounds of workgroups, so one whose pairs took long no longer leaves its
+    // CU half empty until the kernel ends (one round: 4.6 of 8 waves/SIMD on average)
+    for (uint32_t gj = blockIdx.x; gj < nseg * split; gj += gridDim.x) {
+        const uint32_t g = gj / split, part = gj % split;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t run = 0;
@@ -1912,7 +1917,8 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         __syncthreads();
         const uint32_t m = s_mp[PAIR_WAVES];
-        for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) {
+        const uint32_t k0 = (uint32_t)((uint64_t)m * part / split), k1 = (uint32_t)((uint64_t)m * (part + 1) / split);
+        for (uint32_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
             int w = 0;
             while (w + 1 < PAIR_WAVES && s_mp[w + 1] <= k) ++w;
             const uint32_t i = matched[(uint64_t)(g * PAIR_WAVES + w) * seg + (k - s_mp[w])];
@@ -4103,6 +4109,7 @@ struct pii_engine {
     uint32_t* mcount = nullptr;   // matched pairs per k_pair_first wavefront segment
     FirstCont* cont = nullptr;
     uint32_t n_seg = 0;
+    uint32_t eval_split = 2;        // k_pair_eval work units per k_pair_first workgroup (PII_EVAL_SPLIT)
     struct Call {
         const uint8_t* text;
         const uint64_t* offs;
@@ -4607,15 +4614,16 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         return rc;
     if (n_utt > 0 && n_chunks > 0) {
         if (e->img_eval_rg.d) {
-            k_pair_eval<false, true><<<e->n_seg, PAIR_BLOCK, e->img_eval_rg.lds(), st>>>(
+            k_pair_eval<false, true><<<e->n_seg * e->eval_split, PAIR_BLOCK, e->img_eval_rg.lds(), st>>>(
                 e->img_eval_rg.d, e->img_eval_rg.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
                 e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), R.rule_off,
-                R.rule_ids);
+                R.rule_ids, e->eval_split);
         } else {
-            (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(),
-                                                                             st>>>(
+            (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg * e->eval_split, PAIR_BLOCK,
+                                                                             e->img_eval.lds(), st>>>(
                 e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
-                e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), nullptr, nullptr);
+                e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), nullptr, nullptr,
+                e->eval_split);
         }
         const bool xg = e->img_sel_rg.d != nullptr;
         const DevImage& isel = xg ? e->img_sel_rg : e->img_sel;
@@ -5327,7 +5335,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             e->n_cu = prop.multiProcessorCount;
-        e->n_seg = 2 * (uint32_t)e->n_cu;      // two 1024-thread pair workgroups per CU
+        // k_pair_first: two 1024-thread workgroups per CU, one round (2 or 4 rounds: 160 -> 165 / 164 µs,
+        // and k_pair_eval slower on the smaller segments)
+        e->n_seg = 2 * (uint32_t)e->n_cu;
+        if (const char* v = std::getenv("PII_EVAL_SPLIT")) e->eval_split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
     e->scan_lds = SCAN_TD_BASE + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4 + SCAN_SPREAD_BYTES;
