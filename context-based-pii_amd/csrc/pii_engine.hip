@@ -508,7 +508,9 @@ __global__ __launch_bounds__(HALO_BLOCK) void k_halo(const RulesDev R, const Geo
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
 __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* __restrict__ lane_pos,
                                                    uint64_t* __restrict__ words) {
-    __shared__ int64_t s_off[4][PAIRS_UCAP + 1];
+    // (batch-relative offsets fit 32 bits: 16 KiB of LDS per workgroup instead of 32 leaves the
+    // kernel at its register occupancy, 7 waves/SIMD, instead of 4)
+    __shared__ uint32_t s_off[4][PAIRS_UCAP + 1];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t cw0 = c - lane;
@@ -517,12 +519,12 @@ __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* 
     const uint32_t U0 = cw0 < g.n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
     const uint32_t U1 = cw0 < g.n_chunks ? min(g.first_utt[cw1] + 1u, g.n_utt) : 0u;
     const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
-    int64_t* so = s_off[wv];
+    uint32_t* so = s_off[wv];
     if (staged && cw0 < g.n_chunks)
-        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = g_off(g, U0 + k);
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)g_off(g, U0 + k);
     __syncthreads();
     if (c >= g.n_chunks) return;
-    auto uoff = [&](int64_t u) { return staged ? so[u - U0] : g_off(g, (uint32_t)u); };
+    auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : g_off(g, (uint32_t)u); };
     const Lane L = g_lane(g, c);
     const uint32_t top = scan_top(g, L);
     if (top <= L.lo) return;
