@@ -884,7 +884,7 @@ SCAN_GROUP_BYTES = 62 * 1024    # D table of a scan group >= 1 that keeps 16-bit
 SCAN_WIDE_BYTES = 124 * 1024    # a WIDE group >= 1 (engine: rows padded to 4 entries, entries = offset / 2,
                                 # one workgroup per CU): up to 64k transitions
 SPILL_PREFIX = 10               # prefix of the built-ins moved out of group 0 (plan_scan_groups)
-SCAN_GROUPS_MAX = 8             # k_pairs merges at most this many per-group event lists per lane
+SCAN_GROUPS_MAX = 8             # k_pairs_merge merges at most this many per-group event lists per lane
 DICT_SCAN_PREFIX = 4            # SCAN prefix of dictionary infoTypes (Rules)
 
 

@@ -684,7 +684,8 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 // HK = false: a SCAN group >= 1, whose K is the never-accepting one-row stub -- K is not stepped (its
 // row stays the start row, its transition is the stub's class-0 entry), one LDS read less per byte
 // NT: 768 threads (two workgroups per CU with tables <= 80 KiB, 6 waves / SIMD), or SCAN_BLOCK_WIDE for
-// a WIDE group's table (one workgroup per CU: 16 waves instead of 12)
+// a WIDE group's table (one workgroup per CU: 16 waves instead of 12).  (256-thread workgroups for the
+// window re-scan's small steps, to reach every CU instead of 123: 67 -> 73 us, not kept)
 constexpr int SCAN_BLOCK_WIDE = 1024;
 template <bool HK, int NT = SCAN_BLOCK>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? 6 : 4, NT == SCAN_BLOCK ? 6 : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
@@ -1275,100 +1276,59 @@ constexpr int PAIRS_BLOCK = 256;
 //
 // MULTI (a rule set split over several SCAN groups, config 5): every group's k_scan pass wrote its
 // own per-lane event list (descending position, arena g at ev + g * ev_stride), counted per group by
-// the flat pass.  The write pass here merges the lists by position, a tie going to the higher group
-// first so that, the queue being filled back to front, group 0 (built-ins and excluders) comes first
-// among one start's pairs; k_expand then writes the pairs.  (Measured alternative: this walk
-// assigning only each event's first pair index, the records then written by the flat pass per
-// group -- 2.30 + 1.61 ms against 3.19 + 0.39 ms here; the merge walk itself is the cost.)
+// the flat pass.  The write pass (k_pairs_merge) merges the lists by position, a tie going to the
+// higher group first so that, the queue being filled back to front, group 0 (built-ins and
+// excluders) comes first among one start's pairs; k_expand then writes the pairs.  (A per-lane walk
+// of the merge -- one thread per lane, two dependent global loads per event -- took 1026 us at config
+// 5; the rank form below 597 us.)
 constexpr int SCAN_GROUPS_MAX = 8;
 struct AccTabs {                 // per SCAN group, by D transition index:
     const uint16_t* accid[SCAN_GROUPS_MAX];   // global D accept-set id
     const uint16_t* npair[SCAN_GROUPS_MAX];   // pairs of that accept set
 };
 
-template <bool WRITE, bool MULTI>
-__global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const Geo g,
-                                               const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
-                                               const uint8_t* __restrict__ role, int32_t* __restrict__ kw,
-                                               EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
-                                               uint64_t pair_cap, uint64_t ev_cap,
-                                               const uint64_t* __restrict__ lane_pair,
-                                               const uint64_t* __restrict__ lane_ev,
-                                               uint32_t* __restrict__ lane_np, uint32_t* __restrict__ err,
-                                               uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
-                                               const AccTabs acct, uint32_t* __restrict__ lane_evn) {
-    __shared__ uint32_t s_off[PAIRS_BLOCK / 64][PAIRS_UCAP + 1];
-    __shared__ uint32_t s_acc_off[256];
-    if (*err & ERR_ARGS) return;
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t n_chunks = g.n_chunks;
-    const bool valid = c < n_chunks;
-    const uint64_t* __restrict__ offs = g.offs;
-    const int64_t base = (int64_t)g.base;
-    // small accept-set tables (<= 256 sets; larger rule sets read them from global memory)
-    const uint32_t n_dacc = R.n_dacc;
-    for (uint32_t i = threadIdx.x; i <= n_dacc && i < 256; i += PAIRS_BLOCK) s_acc_off[i] = R.d_acc_off[i];
-    // the wavefront's utterances [U0, U1] (from one before its first lane's first start: a cut row)
-    const uint32_t cw0 = c - lane;
-    const uint32_t cw1 = min(cw0 + 64, n_chunks);
-    const uint32_t U0 = cw0 < n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
-    const uint32_t U1 = cw0 < n_chunks ? g.first_utt[cw1] : 0u;
-    const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
-    uint32_t* so = s_off[wv];
-    if (staged && cw0 < n_chunks)
-        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)((int64_t)offs[U0 + k] - base);
-    __syncthreads();
-    const bool small_acc = n_dacc < 256;
-    auto acc_off = [&](uint32_t a) { return small_acc ? s_acc_off[a] : R.d_acc_off[a]; };
-    auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : (int64_t)offs[u] - base; };
+// MULTI write pass, rank form.  A wavefront owns MERGE_LPW consecutive lanes and stages every event
+// of every group of its lanes in LDS (position, pairs | accept set, running pair count within the
+// lane's group list), loaded flattened (64 events per load instruction, as in k_pairs_flat).  An
+// event's place k in its lane's merged order (descending position, a tie going to the higher group
+// -- the walk above) is its index in its own list plus, per other group, a binary search of that
+// group's list in LDS; its first pair is the lane's top minus the pairs of every event up to and
+// including it.  So no lane walks a serial chain of dependent global loads.  A wavefront whose
+// lanes hold more than `evw_cap` events walks them one by one instead (merge_walk).
+#ifndef MERGE_LPW
+#define MERGE_LPW 8
+#endif
+#ifndef MERGE_EVW
+#define MERGE_EVW 512
+#endif
+constexpr int MERGE_WAVES = 4;
+constexpr int MERGE_UCAP = 512;      // utterances of its lanes a wavefront stages
+static_assert(MERGE_LPW <= 64 && (MERGE_LPW & (MERGE_LPW - 1)) == 0, "lanes per wavefront: a power of two <= 64");
+static_assert(MERGE_EVW % 64 == 0, "staged events: whole 64-event chunks");
 
-    // the lane's events in descending position: one list, or the merge of the groups' lists
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// one lane's events in merged order, walked (the over-capacity fallback of k_pairs_merge)
+__device__ void merge_walk(const Geo& g, const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
+                           uint32_t c, uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
+                           const AccTabs& acct, uint64_t top, uint64_t evb, EvLoc* __restrict__ evloc,
+                           EvPairs* __restrict__ evpairs) {
+    const Lane L = g_lane(g, c);
+    const uint64_t eb = ev_base(L, c);
+    uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX], hp[SCAN_GROUPS_MAX];
     uint32_t cnt = 0;
-    int64_t u_top = 0;
-    Lane L{};
-    uint64_t evoff = 0;
-    if (valid) {
-        if (MULTI) {
-            for (uint32_t q = 0; q < n_groups; ++q) cnt += lane_cnt[(uint64_t)q * cnt_stride + c];
-        } else {
-            cnt = lane_cnt[c];
-        }
-    }
-    if (cnt) {
-        L = g_lane(g, c);
-        evoff = ev_base(L, c);
-        u_top = (int64_t)L.u1 - 1;
-    }
-    const Event* evl = ev + evoff;
-    uint32_t k1 = 0;                        // single list: next index
-    Event En = (!MULTI && cnt) ? evl[0] : Event{};
-    // the groups' list heads in registers (position, sd | sk << 16); the merge step is branch-free:
-    // the winning group's head, table and next event are picked with select trees, so every step
-    // issues one accept-set load and one event load for the whole wavefront (a per-group branch
-    // would issue them once per group, each with a few lanes active)
-    uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX], hp[SCAN_GROUPS_MAX], hx[SCAN_GROUPS_MAX];
-    if (MULTI) {
 #pragma unroll
-        for (int q = 0; q < SCAN_GROUPS_MAX; ++q) {
-            gk[q] = 0;
-            gn[q] = (cnt && (uint32_t)q < n_groups) ? lane_cnt[(uint64_t)q * cnt_stride + c] : 0u;
-            const Event H = gn[q] ? evl[(uint64_t)q * ev_stride] : Event{};
-            hp[q] = H.pos;
-            hx[q] = (uint32_t)H.sd | (uint32_t)H.sk << 16;
-        }
+    for (int q = 0; q < SCAN_GROUPS_MAX; ++q) {
+        gk[q] = 0;
+        gn[q] = (uint32_t)q < n_groups ? lane_cnt[(uint64_t)q * cnt_stride + c] : 0u;
+        hp[q] = gn[q] ? ev[(uint64_t)q * ev_stride + eb].pos : 0u;
+        cnt += gn[q];
     }
-    // next event (E) and its D accept set; k0: it is group 0's (the keyword automaton's group)
-    auto next = [&](Event& E, uint32_t& acc, bool& k0) {
-        if (!MULTI) {
-            E = En;
-            if (k1 + 1 < cnt) En = evl[k1 + 1];
-            ++k1;
-            acc = R.d_accid[E.sd];
-            k0 = true;
-            return;
-        }
-        uint32_t best = 0, bp = 0;
+    uint64_t w = top;
+    int64_t u = (int64_t)L.u1 - 1;
+    int64_t s_u = g_off(g, (uint32_t)u), e_u = g_off(g, (uint32_t)u + 1);
+    for (uint32_t k = 0; k < cnt; ++k) {
+        uint32_t best = 0, bp = 0, kb = 0;
         bool any = false;
 #pragma unroll
         for (int q = SCAN_GROUPS_MAX - 1; q >= 0; --q)
@@ -1377,76 +1337,233 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs(const RulesDev R, const G
                 bp = hp[q];
                 any = true;
             }
-        uint32_t x = 0, kb = 0, nb = 0;
+        const uint16_t* accid = acct.accid[0];
+        const uint16_t* npair = acct.npair[0];
 #pragma unroll
         for (int q = 0; q < SCAN_GROUPS_MAX; ++q)
             if ((uint32_t)q == best) {
-                x = hx[q];
-                kb = gk[q] + 1u;
-                nb = gn[q];
+                kb = gk[q];
+                accid = acct.accid[q];
+                npair = acct.npair[q];
             }
-        E.pos = bp;
-        E.sd = (uint16_t)(x & 0xffffu);
-        E.sk = (uint16_t)(x >> 16);
-        const bool b0 = best & 1u, b1 = best & 2u, b2 = best & 4u;
-        const uint16_t* t01 = b0 ? acct.accid[1] : acct.accid[0];
-        const uint16_t* t23 = b0 ? acct.accid[3] : acct.accid[2];
-        const uint16_t* t45 = b0 ? acct.accid[5] : acct.accid[4];
-        const uint16_t* t67 = b0 ? acct.accid[7] : acct.accid[6];
-        const uint16_t* tab = b2 ? (b1 ? t67 : t45) : (b1 ? t23 : t01);
-        acc = tab[E.sd];
-        Event H{};
-        if (kb < nb) H = evl[(uint64_t)best * ev_stride + kb];
+        const uint64_t gb = (uint64_t)best * ev_stride + eb;
+        const Event E = ev[gb + kb];
 #pragma unroll
         for (int q = 0; q < SCAN_GROUPS_MAX; ++q)
-            if ((uint32_t)q == best) {           // register updates only (selects)
-                gk[q] = kb;
-                hp[q] = H.pos;
-                hx[q] = (uint32_t)H.sd | (uint32_t)H.sk << 16;
+            if ((uint32_t)q == best) {
+                gk[q] = kb + 1;
+                hp[q] = kb + 1 < gn[q] ? ev[gb + kb + 1].pos : 0u;
             }
-        k0 = best == 0;
-    };
-
-    static_assert(WRITE && MULTI, "counting is k_pairs_flat<false>, one SCAN group k_pairs_flat<true>");
-    if (!valid) return;
-    const uint32_t np = lane_np[c];
-    const uint64_t my = lane_pair[c];
-    const uint64_t evb = lane_ev[c];
-    if (cnt == 0) return;                 // (every event gets its EvPairs record, even with no pairs)
-    if (my + np > pair_cap || evb + cnt > ev_cap) {
-        atomicOr(err, (uint32_t)ERR_QUEUE);
-        return;
-    }
-    // pass 2: write back to front -> ascending by start
-    uint64_t w = my + np;
-    int64_t u = u_top;
-    int64_t s_u = uoff(u);
-    int64_t e_u = uoff(u + 1);
-    for (uint32_t k = 0; k < cnt; ++k) {
-        Event E;
-        uint32_t acc;
-        bool k0;
-        next(E, acc, k0);
         const int64_t pos = E.pos;
         while (pos < s_u) {
             --u;
             e_u = s_u;
-            s_u = uoff(u);
+            s_u = g_off(g, (uint32_t)u);
         }
-        const uint32_t a0 = acc_off(acc), a1 = acc_off(acc + 1);
-        w -= a1 - a0;
+        const uint32_t n = npair[E.sd];
+        w -= n;
         EvPairs ep;
         ep.first = (uint32_t)w;
-        ep.acc = (uint16_t)acc;
-        ep.n = (uint16_t)(a1 - a0);
+        ep.acc = accid[E.sd];
+        ep.n = (uint16_t)n;
         evpairs[evb + k] = ep;
-        if (a1 == a0) continue;
+        if (n == 0) continue;
         EvLoc Lc;
         Lc.u = (uint32_t)u;
         Lc.s = (uint32_t)pos;
         Lc.ustart = (uint32_t)s_u;
         Lc.uend = (uint32_t)e_u;
         evloc[evb + k] = Lc;
+    }
+}
+
+__global__ __launch_bounds__(MERGE_WAVES * 64) void k_pairs_merge(const Geo g, const Event* __restrict__ ev,
+                                                           const uint32_t* __restrict__ lane_cnt,
+                                                           EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
+                                                           uint64_t pair_cap, uint64_t ev_cap,
+                                                           const uint64_t* __restrict__ lane_pair,
+                                                           const uint64_t* __restrict__ lane_ev,
+                                                           const uint32_t* __restrict__ lane_np,
+                                                           uint32_t* __restrict__ err, uint32_t n_groups,
+                                                           uint64_t ev_stride, uint32_t cnt_stride, const AccTabs acct,
+                                                           uint32_t evw_cap) {
+    __shared__ uint32_t s_pos[MERGE_WAVES][MERGE_EVW];
+    __shared__ uint32_t s_na[MERGE_WAVES][MERGE_EVW];      // pairs | accept set << 16
+    __shared__ uint32_t s_pn[MERGE_WAVES][MERGE_EVW];      // pairs of the lane's group list up to here
+    __shared__ uint32_t s_lb[MERGE_WAVES][SCAN_GROUPS_MAX * MERGE_LPW + 1];   // list (q, l) start, q-major
+    __shared__ uint32_t s_uo[MERGE_WAVES][MERGE_UCAP + 1];
+    if (*err & ERR_ARGS) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t n_chunks = g.n_chunks;
+    const uint32_t cw0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_LPW;
+    if (cw0 >= n_chunks) return;                      // (no workgroup barriers below)
+    const uint32_t nl = min((uint32_t)MERGE_LPW, n_chunks - cw0);
+    const bool own = (uint32_t)lane < nl;             // lanes 0..nl-1 own scan lanes cw0 + lane
+    const uint32_t c = cw0 + lane;
+    const int64_t base = (int64_t)g.base;
+    // the owners' lane records and per-group event counts, and the wavefront's row range: all loads
+    // issued together (independent)
+    uint32_t cq[SCAN_GROUPS_MAX], tot = 0, u0 = 0, u1 = 0;
+    uint64_t eb = 0, top = 0, evb = 0;
+    const uint32_t U0 = max(g.first_utt[cw0], 1u) - 1u, U1 = g.first_utt[cw0 + nl];
+    Lane L{};
+    uint64_t lp = 0, le = 0;
+    uint32_t lnp = 0;
+    if (own) {
+        L = g_lane(g, c);
+        lp = lane_pair[c];
+        lnp = lane_np[c];
+        le = lane_ev[c];
+    }
+#pragma unroll
+    for (int r = 0; r < SCAN_GROUPS_MAX; ++r) {
+        cq[r] = (own && (uint32_t)r < n_groups) ? lane_cnt[(uint64_t)r * cnt_stride + c] : 0u;
+        tot += cq[r];
+    }
+    if (tot) {
+        eb = ev_base(L, c);
+        u0 = L.u0;
+        u1 = L.u1;
+        top = lp + lnp;
+        evb = le;
+    }
+    const bool over = tot && (top > pair_cap || evb + tot > ev_cap);
+    if (__any(over)) {
+        if (lane == 0) atomicOr(err, (uint32_t)ERR_QUEUE);
+        return;
+    }
+    // list starts, q-major over the wavefront's lanes (an exclusive scan of the counts)
+    uint32_t* lbf = s_lb[wv];
+    uint32_t T = 0;
+#pragma unroll
+    for (int r = 0; r < SCAN_GROUPS_MAX; ++r) {
+        uint32_t incl = cq[r];
+#pragma unroll
+        for (int d = 1; d < MERGE_LPW; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        if (lane < MERGE_LPW) lbf[r * MERGE_LPW + lane] = T + incl - cq[r];
+        T += __shfl(incl, MERGE_LPW - 1);
+    }
+    if (T == 0) return;
+    if (T > evw_cap) {                                // too many events to stage: walk them
+        if (own && tot) merge_walk(g, ev, lane_cnt, c, n_groups, ev_stride, cnt_stride, acct, top, evb, evloc, evpairs);
+        return;
+    }
+    if (lane == 0) lbf[SCAN_GROUPS_MAX * MERGE_LPW] = T;
+    // utterance offsets of the wavefront's lanes (rows [U0, U1], from one before the first lane's
+    // first start: a cut row)
+    const bool staged = U1 - U0 <= (uint32_t)MERGE_UCAP;
+    uint32_t* so = s_uo[wv];
+    if (staged)
+        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)((int64_t)g.offs[U0 + k] - base);
+    auto uoff = [&](uint32_t u) { return staged ? so[u - U0] : (uint32_t)((int64_t)g.offs[u] - base); };
+    uint32_t* sp = s_pos[wv];
+    uint32_t* sa = s_na[wv];
+    uint32_t* sn = s_pn[wv];
+    wave_lds_sync();
+    const uint32_t NL = n_groups * MERGE_LPW;
+    // event f of the wavefront lies in list li = the last one whose start is <= f (an empty list
+    // shares its start with the next one)
+    auto list_of = [&](uint32_t f) {
+        uint32_t li = 0;
+#pragma unroll
+        for (uint32_t st = SCAN_GROUPS_MAX * MERGE_LPW / 2; st >= 1; st >>= 1)
+            if (li + st < NL && lbf[li + st] <= f) li += st;
+        return li;
+    };
+    // stage every event (position, pairs | accept set), flattened over the lists; all 64-event
+    // chunks of a wavefront in one round, their loads issued together
+    constexpr int CH = MERGE_EVW / 64;
+    for (uint32_t f0 = 0; f0 < T; f0 += CH * 64) {
+        Event E[CH];
+        uint32_t fq[CH];
+#pragma unroll
+        for (int r = 0; r < CH; ++r) {
+            const uint32_t f = f0 + r * 64 + lane;
+            const uint32_t li = list_of(f);
+            const uint32_t q = li / MERGE_LPW, l = li % MERGE_LPW;
+            const uint64_t o_eb = __shfl(eb, (int)l);
+            fq[r] = q;
+            E[r] = Event{};
+            if (f < T) E[r] = ev[(uint64_t)q * ev_stride + o_eb + (f - lbf[li])];
+        }
+#pragma unroll
+        for (int r = 0; r < CH; ++r) {
+            const uint32_t f = f0 + r * 64 + lane;
+            if (f < T) {
+                const uint16_t* npair = acct.npair[0];
+                const uint16_t* accid = acct.accid[0];
+#pragma unroll
+                for (int q = 1; q < SCAN_GROUPS_MAX; ++q)
+                    if ((uint32_t)q == fq[r]) {
+                        npair = acct.npair[q];
+                        accid = acct.accid[q];
+                    }
+                sp[f] = E[r].pos;
+                sa[f] = (uint32_t)npair[E[r].sd] | (uint32_t)accid[E[r].sd] << 16;
+            }
+        }
+    }
+    wave_lds_sync();
+    // running pair count of every list (owners, in LDS)
+    if (own && tot)
+        for (uint32_t q = 0; q < n_groups; ++q) {
+            const uint32_t b = lbf[q * MERGE_LPW + lane], n = lbf[q * MERGE_LPW + lane + 1] - b;
+            uint32_t run = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                run += sa[b + i] & 0xffffu;
+                sn[b + i] = run;
+            }
+        }
+    wave_lds_sync();
+    // every event's merged rank and first pair, flattened over the lists.  (Permuting the records
+    // through LDS so that the stores land in slot order measured slower: 597 -> 617 us at config 5.)
+    for (uint32_t f0 = 0; f0 < T; f0 += 64) {
+        const uint32_t f = f0 + lane;
+        const bool act = f < T;
+        const uint32_t li = list_of(f);
+        const uint32_t q = li / MERGE_LPW, ow = li % MERGE_LPW;
+        const uint64_t o_top = __shfl(top, (int)ow), o_evb = __shfl(evb, (int)ow);
+        const uint32_t o_u0 = __shfl(u0, (int)ow), o_u1 = __shfl(u1, (int)ow);
+        if (!act) continue;
+        const uint32_t pos = sp[f], na = sa[f];
+        uint32_t k = f - lbf[li];                          // index in its own list
+        uint32_t pn = sn[f];                               // pairs up to and including it, own list
+        for (uint32_t q2 = 0; q2 < n_groups; ++q2) {       // events of q2 placed before this one
+            if (q2 == q) continue;
+            const uint32_t b2 = lbf[q2 * MERGE_LPW + ow];
+            uint32_t lo = 0, hi = lbf[q2 * MERGE_LPW + ow + 1] - b2;
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                const uint32_t p2 = sp[b2 + m];
+                if (p2 > pos || (p2 == pos && q2 > q)) lo = m + 1;
+                else hi = m;
+            }
+            k += lo;
+            if (lo) pn += sn[b2 + lo - 1];
+        }
+        const uint32_t n = na & 0xffffu;
+        EvPairs ep;
+        ep.first = (uint32_t)(o_top - pn);
+        ep.acc = (uint16_t)(na >> 16);
+        ep.n = (uint16_t)n;
+        evpairs[o_evb + k] = ep;
+        if (n) {
+            uint32_t lo = o_u0, hi = o_u1 - 1;           // the event's row: last u with start <= pos
+            while (lo < hi) {
+                const uint32_t m = (lo + hi + 1) >> 1;
+                if (uoff(m) <= pos) lo = m;
+                else hi = m - 1;
+            }
+            EvLoc Lc;
+            Lc.u = lo;
+            Lc.s = pos;
+            Lc.ustart = uoff(lo);
+            Lc.uend = uoff(lo + 1);
+            evloc[o_evb + k] = Lc;
+        }
     }
 }
 
@@ -2865,48 +2982,61 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
     if (total_p == 0) return;
     uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
     const int64_t span = out_hi - out_lo;
-    for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
-        const int64_t r0 = q * 16 - omis - out_lo;      // tile-relative output offset of byte 0
-        const int b_lo = r0 < 0 ? (int)-r0 : 0;          // valid bytes [b_lo, b_hi) of the block
-        const int b_hi = r0 + 16 > span ? (int)(span - r0) : 16;
-        uint32_t pi;
+    // a block's first piece is loaded before the loop over its further pieces (those are rare); two
+    // or four blocks per thread in flight measured slower (more VGPRs, no fewer stalls)
+    struct Blk {
+        int64_t r0;
+        int b_lo, b_hi, lo, hi;
+        uint32_t pi, qs, qe;
+        uint64_t qsrc;
+        uint4 w;
+    };
+    auto begin = [&](Blk& k, int64_t q) {
+        k.r0 = q * 16 - omis - out_lo;                   // tile-relative output offset of byte 0
+        k.b_lo = k.r0 < 0 ? (int)-k.r0 : 0;              // valid bytes [b_lo, b_hi) of the block
+        k.b_hi = k.r0 + 16 > span ? (int)(span - k.r0) : 16;
         if (table) {
-            pi = s_bp[q - q_lo];
+            k.pi = s_bp[q - q_lo];
         } else {
-            const uint32_t rs = (uint32_t)(r0 + b_lo);
+            const uint32_t rs = (uint32_t)(k.r0 + k.b_lo);
             uint32_t lo_i = 0, hi_i = total_p - 1;       // last piece with s_pout <= rs
             while (lo_i < hi_i) {
                 const uint32_t mid = (lo_i + hi_i + 1) >> 1;
                 if (s_pout[mid] <= rs) lo_i = mid;
                 else hi_i = mid - 1;
             }
-            pi = lo_i;
+            k.pi = lo_i;
         }
-        uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
-        uint64_t qsrc = s_psrc[pi];
+        k.qs = s_pout[k.pi];
+        k.qe = s_pout[k.pi + 1];
+        k.qsrc = s_psrc[k.pi];
+        k.lo = max(k.b_lo, (int)((int64_t)k.qs - k.r0));
+        k.hi = min(k.b_hi, (int)((int64_t)k.qe - k.r0));
+        k.w = make_uint4(0, 0, 0, 0);
+        if (k.hi > k.lo) k.w = load16(reinterpret_cast<const uint8_t*>(k.qsrc) + (k.r0 - (int64_t)k.qs), k.lo, k.hi);
+    };
+    auto merge = [](uint4& v, const uint4& w, int lo, int hi) {
+        v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
+        v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
+        v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
+        v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
+    };
+    auto finish = [&](Blk& k, int64_t q) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        for (;;) {                                       // pieces overlapping [r0 + b_lo, r0 + b_hi)
-            const int lo = max(b_lo, (int)((int64_t)qs - r0));
-            const int hi = min(b_hi, (int)((int64_t)qe - r0));
-            if (hi > lo) {
-                const int64_t delta = r0 - (int64_t)qs;       // block byte 0 <-> piece byte delta
-                const uint4 w = load16(reinterpret_cast<const uint8_t*>(qsrc) + delta, lo, hi);
-                if (lo == 0 && hi == 16) {
-                    v = w;
-                } else {
-                    v.x |= w.x & (bytemask(hi) & ~bytemask(lo));
-                    v.y |= w.y & (bytemask(hi - 4) & ~bytemask(lo - 4));
-                    v.z |= w.z & (bytemask(hi - 8) & ~bytemask(lo - 8));
-                    v.w |= w.w & (bytemask(hi - 12) & ~bytemask(lo - 12));
-                }
-            }
-            if ((int64_t)qe >= r0 + b_hi) break;
-            ++pi;
-            qs = qe;
-            qe = s_pout[pi + 1];
-            qsrc = s_psrc[pi];
+        if (k.hi > k.lo) {
+            if (k.lo == 0 && k.hi == 16) v = k.w;
+            else merge(v, k.w, k.lo, k.hi);
         }
-        if (b_lo == 0 && b_hi == 16) {
+        while ((int64_t)k.qe < k.r0 + k.b_hi) {          // pieces overlapping [r0 + b_lo, r0 + b_hi)
+            ++k.pi;
+            k.qs = k.qe;
+            k.qe = s_pout[k.pi + 1];
+            k.qsrc = s_psrc[k.pi];
+            const int lo = max(k.b_lo, (int)((int64_t)k.qs - k.r0));
+            const int hi = min(k.b_hi, (int)((int64_t)k.qe - k.r0));
+            if (hi > lo) merge(v, load16(reinterpret_cast<const uint8_t*>(k.qsrc) + (k.r0 - (int64_t)k.qs), lo, hi), lo, hi);
+        }
+        if (k.b_lo == 0 && k.b_hi == 16) {
             u32x4_t nv = {v.x, v.y, v.z, v.w};          // (streaming stores: -15 us per config-2 step)
             __builtin_nontemporal_store(nv, reinterpret_cast<u32x4_t*>(op + q));
         } else {
@@ -2914,8 +3044,13 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
             const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 16; ++j)
-                if (j >= b_lo && j < b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
+                if (j >= k.b_lo && j < k.b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
         }
+    };
+    for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
+        Blk k;
+        begin(k, q);
+        finish(k, q);
     }
 }
 
@@ -4070,7 +4205,7 @@ struct pii_engine {
     std::vector<RulesDev> sg;
     std::vector<size_t> sg_lds;
     AccTabs acct{};
-    uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs<.., MULTI>)
+    uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs_merge)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
     DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
     DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
@@ -4111,7 +4246,8 @@ struct pii_engine {
     uint32_t* mcount = nullptr;   // matched pairs per k_pair_first wavefront segment
     FirstCont* cont = nullptr;
     uint32_t n_seg = 0;
-    uint32_t eval_split = 2;        // k_pair_eval work units per k_pair_first workgroup (PII_EVAL_SPLIT)
+    uint32_t eval_split = 2;           // k_pair_eval work units per k_pair_first workgroup (PII_EVAL_SPLIT)
+    uint32_t merge_cap = MERGE_EVW;    // k_pairs_merge: events a wavefront stages (PII_MERGE_CAP; 0: walk)
     struct Call {
         const uint8_t* text;
         const uint64_t* offs;
@@ -4522,10 +4658,10 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             // context-only call need the keyword groups of the count pass only, and cannot overflow it)
             if (!pair_first) {
             } else if (multi) {
-                k_pairs<true, true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                 e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
-                                                                 e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct,
-                                                                 e->lane_evn);
+                const uint32_t lpb = MERGE_WAVES * MERGE_LPW;
+                k_pairs_merge<<<(n_chunks + lpb - 1) / lpb, MERGE_WAVES * 64, 0, st>>>(
+                    g, e->ev, e->lane_cnt, e->evloc, e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev,
+                    e->lane_np, e->d_err, ns, es, cs, e->acct, e->merge_cap);
                 k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
             } else {
                 k_pairs_flat<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
@@ -5341,6 +5477,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         // and k_pair_eval slower on the smaller segments)
         e->n_seg = 2 * (uint32_t)e->n_cu;
         if (const char* v = std::getenv("PII_EVAL_SPLIT")) e->eval_split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+        if (const char* v = std::getenv("PII_MERGE_CAP")) e->merge_cap = (uint32_t)std::max(0, std::min(MERGE_EVW, std::atoi(v)));
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
     }
     e->scan_lds = SCAN_TD_BASE + (size_t)(R.SD * R.CDs / 2) * 4 + (size_t)(R.SK * R.CKs / 2) * 4 + SCAN_SPREAD_BYTES;

@@ -187,3 +187,28 @@ def test_config5_long_rows(c5, c5_comp, c5_oracle):
         got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"])) for s in res.spans[m]]
         assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], i
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["0", "40"])
+def test_config5_merge_walk_fallback(c5, c5_comp, c5_oracle, monkeypatch, cap):
+    """k_pairs_merge stages a wavefront's events of every SCAN group and ranks them in LDS; a
+    wavefront with more events than PII_MERGE_CAP walks its lanes instead.  cap 0: every wavefront
+    walks; cap 40: the two forms side by side in one call.  Bit-exact vs the oracle either way."""
+    from oracle import pii_oracle as O
+    E = pkg("engine")
+    c, _ = c5
+    rows = _conversations(c, 120, 8, 19)
+    monkeypatch.setenv("PII_MERGE_CAP", cap)
+    eng = E.Engine(c5_comp.blob, device=0, n_conv_slots=1 << 8)
+    try:
+        res = eng.scan_redact([x[2] for x in rows], [x[0] for x in rows], [x[1] for x in rows],
+                              [x[3] for x in rows])
+        exp = O.process_rows(rows, c5_oracle)
+        for i, (red, fs, _, _) in enumerate(exp):
+            assert res.text(i) == red, i
+            m = res.spans["utt"] == i
+            got = [(int(s["start"]), int(s["end"]), int(s["info_type"]), int(s["likelihood"])) for s in res.spans[m]]
+            assert got == [(f.start, f.end, f.type_id, f.likelihood) for f in fs], i
+    finally:
+        eng.close()
