@@ -1847,6 +1847,11 @@ __device__ __forceinline__ const uint8_t* load_image(const uint4* __restrict__ i
 // segment of `matched` and the runs still alive after one 16-byte window into the same segment of
 // `cont`.  The workgroup then finishes all its continuations densely, so one long run no longer holds
 // 63 idle lanes; their matches are appended through LDS counters.
+//
+// GI (the image past LDS, read in place from L2): the automata of the first `p_hot` patterns (the
+// shipped built-in types come first: half of config 5's pairs) are copied into LDS as a second image
+// `himg`, and a pair of those patterns steps them there -- fewer L2 requests, the bound of this
+// kernel at config 5.  (Pointers are then generic: a lane's loads go to LDS or L2 by its pattern.)
 template <bool GI>
 __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_first(const uint4* __restrict__ img, const LdsImage li,
                                                            const uint8_t* __restrict__ text0,
@@ -1857,7 +1862,9 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
                                                            int32_t* __restrict__ pend, uint32_t* __restrict__ matched,
                                                            FirstCont* __restrict__ cont,
                                                            uint32_t* __restrict__ mcount,
-                                                           const uint32_t* __restrict__ err) {
+                                                           const uint32_t* __restrict__ err,
+                                                           const uint4* __restrict__ himg, const LdsImage hli,
+                                                           uint32_t p_hot) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     __shared__ uint32_t s_mc[PAIR_WAVES], s_cc[PAIR_WAVES + 1];
     if (*err & ERR_ABORT) {
@@ -1867,6 +1874,19 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     const Pool pool{reinterpret_cast<const uint16_t*>(lb + li.off[FI_TRANS]), lb + li.off[FI_CMAP]};
     const int32_t* fdesc = reinterpret_cast<const int32_t*>(lb + li.off[FI_DESC]);
+    Pool hpool = pool;
+    const int32_t* hdesc = fdesc;
+    if (GI && p_hot) {
+        const uint8_t* hb = load_image<false>(himg, hli.total, lds4);
+        hpool = Pool{reinterpret_cast<const uint16_t*>(hb + hli.off[FI_TRANS]), hb + hli.off[FI_CMAP]};
+        hdesc = reinterpret_cast<const int32_t*>(hb + hli.off[FI_DESC]);
+    }
+    // a pattern's automaton: the LDS copy for the leading patterns (GI), else the image's
+    auto tabs = [&](uint32_t p, Pool& pl, const int32_t*& d) {
+        const bool h = GI && p < p_hot;
+        pl = h ? hpool : pool;
+        d = (h ? hdesc : fdesc) + 8 * p;
+    };
     const uint64_t n = min((uint64_t)*pair_count, pair_cap);
     const uint8_t* text = text0 + offs[0];     // pair positions are relative to the batch base
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1882,7 +1902,10 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
         if (i < hi) {
             const PairRes P = pres[i];
             const EvLoc L = evloc[P.ev];
-            e = first_begin(pool, fdesc + 8 * P.p, text + L.ustart, (int)(L.s - L.ustart), (int)(L.uend - L.ustart), r);
+            Pool pl;
+            const int32_t* d;
+            tabs(P.p, pl, d);
+            e = first_begin(pl, d, text + L.ustart, (int)(L.s - L.ustart), (int)(L.uend - L.ustart), r);
             pend[i] = e < 0 ? -1 : e;                 // still-running runs (-2) are completed below
         }
         const uint64_t mm = __ballot(e >= 0), mcn = __ballot(e == -2);
@@ -1923,7 +1946,10 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
         const PairRes P = pres[C.i];
         const EvLoc L = evloc[P.ev];
         FirstState r{C.st, C.pos, C.last};
-        const int e = first_finish(pool, fdesc + 8 * P.p, text + L.ustart, (int)(L.uend - L.ustart), r);
+        Pool pl;
+        const int32_t* d;
+        tabs(P.p, pl, d);
+        const int e = first_finish(pl, d, text + L.ustart, (int)(L.uend - L.ustart), r);
         if (e >= 0) {
             pend[C.i] = e;
             matched[wlo + atomicAdd(&s_mc[w], 1u)] = C.i;
@@ -4162,6 +4188,7 @@ bool parse_blob(const uint8_t* p, size_t n, std::vector<Section>& out) {
 
 // ================================================================================ engine object
 constexpr size_t IMG_LDS_MAX = 160 * 1024;
+constexpr size_t FIRST_HOT_LDS = 78 * 1024;     // k_pair_first<true>'s LDS copy (two 1024-thread workgroups per CU)
 constexpr size_t IMG_LDS_SPLIT = 80 * 1024;    // pair-kernel image size past which its per-(variant, type) lists stay in L2
 struct DevImage {
     LdsImage li{};
@@ -4207,6 +4234,8 @@ struct pii_engine {
     AccTabs acct{};
     uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs_merge)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
+    DevImage img_first_hot;            // img_first past LDS: the automata of its first first_p_hot patterns
+    uint32_t first_p_hot = 0;
     DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
     DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
     int n_cu = 256;
@@ -4688,9 +4717,12 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     HIPCHK(hipEventRecord(e->tev[2], st));
     if (n_utt > 0 && n_chunks > 0 && pair_first) {
         (e->img_first.global ? k_pair_first<true> : k_pair_first<false>)<<<e->n_seg, PAIR_BLOCK,
-                                                                            e->img_first.lds(), st>>>(
+                                                                            e->img_first.global
+                                                                                ? e->img_first_hot.li.total
+                                                                                : e->img_first.lds(),
+                                                                            st>>>(
             e->img_first.d, e->img_first.li, text, offs, pcount, e->pair_cap, e->evloc, e->pres, e->pend, e->matched,
-            e->cont, e->mcount, e->d_err);
+            e->cont, e->mcount, e->d_err, e->img_first_hot.d, e->img_first_hot.li, e->first_p_hot);
         HIPCHK(hipGetLastError());
     }
     return PII_OK;
@@ -5435,6 +5467,36 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
             return fail("rule table upload failed");
+        if (e->img_first.global) {
+            // the leading patterns' FIRST automata (built-in types first) that fit the LDS of two
+            // k_pair_first workgroups per CU, for k_pair_first<true>
+            DfaPool hf;
+            uint32_t ph = 0;
+            for (int p = 0; p < R.P; ++p) {
+                const int32_t* d = fdesc + 8 * p;
+                const size_t tr = hf.trans.size() + 64 + (size_t)d[7] * d[3];
+                const size_t bytes = ((tr * 2 + 15) & ~(size_t)15) + ((hf.cmap.size() + 260 + 15) & ~(size_t)15) +
+                                     (((hf.desc.size() + 8) * 4 + 15) & ~(size_t)15);
+                if (bytes > FIRST_HOT_LDS) break;
+                add_dfa(hf, d, ptrans, pflags, pcmap);
+                ph = (uint32_t)p + 1;
+            }
+            if (const char* v = std::getenv("PII_FIRST_HOT")) ph = std::min<uint32_t>(ph, (uint32_t)std::max(0, std::atoi(v)));
+            if (ph > 0) {
+                hf = DfaPool{};
+                for (uint32_t p = 0; p < ph; ++p) add_dfa(hf, fdesc + 8 * p, ptrans, pflags, pcmap);
+                std::vector<std::pair<const void*, size_t>> ph_parts(FI_N);
+                ph_parts[FI_TRANS] = vec(hf.trans);
+                ph_parts[FI_CMAP] = vec(hf.cmap);
+                ph_parts[FI_DESC] = vec(hf.desc);
+                if (!make_image(ph_parts, e->img_first_hot)) return fail("rule table upload failed");
+                if (e->img_first_hot.li.total > 64 * 1024 &&
+                    hipFuncSetAttribute((const void*)k_pair_first<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)e->img_first_hot.li.total) != hipSuccess)
+                    return fail("cannot raise the LDS limit of k_pair_first");
+                e->first_p_hot = ph;
+            }
+        }
         if (e->img_eval.li.total > IMG_LDS_SPLIT) {
             auto pr = pe;
             pr[EV_ROFF] = std::make_pair((const void*)nullptr, (size_t)0);
@@ -5560,7 +5622,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->ev, e->fd, e->n_ev, e->n_find,
                     e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
-                    e->img_first.d, e->img_eval.d, e->img_eval_rg.d, e->img_sel.d, e->img_sel_rg.d, e->kw, e->ctx, e->agg_v, e->commit,
+                    e->img_first.d, e->img_first_hot.d, e->img_eval.d, e->img_eval_rg.d, e->img_sel.d, e->img_sel_rg.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
                     e->img_wsel.d, e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->wc, e->phot, e->wc_first,
