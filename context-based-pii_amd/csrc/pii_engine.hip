@@ -53,7 +53,7 @@ constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
 constexpr uint32_t BYTES_PER_LANE = BYTES_PER_LANE_N;    // largest scan lane (big batches)
 constexpr uint32_t MIN_LANE_SHIFT = 7;        // smallest scan lane, 128 B (small batches need lanes, not bytes)
 constexpr int KW_NONE = 0x7fff;
-constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_lane_bits, k_pairs)
+constexpr int PAIRS_UCAP = 1024;   // utterances a wavefront stages in LDS (k_pairs_flat)
 
 enum : uint32_t { ERR_CAPACITY = 1, ERR_ORDER = 2, ERR_SLOT = 4, ERR_QUEUE = 8, ERR_RING = 16, ERR_STITCH = 32,
                   ERR_ARGS = 64, ERR_EXT = 128 };
@@ -505,26 +505,53 @@ __global__ __launch_bounds__(HALO_BLOCK) void k_halo(const RulesDev R, const Geo
     }
 }
 
+// The utterance offsets of a wavefront's 64 lanes, staged in LDS as 16-bit offsets from the start of
+// the wavefront's first slice: the rows that START in its slices (at most 64 << sh <= 64 KiB past
+// it); the row before them (a cut row) and the row after them are kept in registers.  Config 5's
+// 57-byte rows are ~1150 per wavefront: 32-bit offsets in the same 16 KiB of LDS held 1024, and
+// k_lane_bits fell back to global loads (183 -> 80 us at config 5).  (k_pairs_flat staged this way
+// measured slower, 213 -> 327 us: its binary searches pay for the range tests; it keeps 32 bits.)
+constexpr int WROWS_CAP = 2048;
+static_assert(BYTES_PER_LANE * 64 <= 65536, "16-bit offsets within a wavefront's slices");
+struct WaveRows {
+    uint16_t* so;
+    int64_t lo;            // relative position of the wavefront's first slice
+    uint32_t uf, ue;       // rows starting in the wavefront's slices: [uf, ue)
+    int64_t o_prev, o_end; // offsets of rows uf - 1 and ue
+    bool staged;
+    __device__ __forceinline__ void stage(const Geo& g, uint32_t cw0, uint32_t cw1, int lane, uint16_t* buf) {
+        so = buf;
+        uf = g.first_utt[cw0];
+        ue = g.first_utt[cw1];
+        lo = g_cpos(g, cw0);
+        staged = ue - uf <= (uint32_t)WROWS_CAP;
+        o_prev = uf > 0 ? g_off(g, uf - 1) : 0;
+        o_end = g_off(g, ue);
+        if (staged)
+            for (uint32_t k = lane; k < ue - uf; k += 64) so[k] = (uint16_t)(g_off(g, uf + k) - lo);
+    }
+    __device__ __forceinline__ int64_t off(const Geo& g, uint32_t u) const {
+        if (u == ue) return o_end;
+        if (staged && u >= uf && u < ue) return lo + so[u - uf];
+        if (u + 1 == uf) return o_prev;
+        return g_off(g, u);
+    }
+};
+
 // one thread per lane; the wavefront stages its utterance offsets in LDS first (coalesced loads)
 __global__ __launch_bounds__(256) void k_lane_bits(const Geo g, const uint32_t* __restrict__ lane_pos,
                                                    uint64_t* __restrict__ words) {
-    // (batch-relative offsets fit 32 bits: 16 KiB of LDS per workgroup instead of 32 leaves the
-    // kernel at its register occupancy, 7 waves/SIMD, instead of 4)
-    __shared__ uint32_t s_off[4][PAIRS_UCAP + 1];
+    // (16 KiB of LDS per workgroup leaves the kernel at its register occupancy, 7 waves/SIMD)
+    __shared__ uint16_t s_off[4][WROWS_CAP];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t cw0 = c - lane;
     const uint32_t cw1 = min(cw0 + 64, g.n_chunks);
-    // the wavefront's utterances [U0, U1] (one before its first lane's first start: a cut row)
-    const uint32_t U0 = cw0 < g.n_chunks ? max(g.first_utt[cw0], 1u) - 1u : 0u;
-    const uint32_t U1 = cw0 < g.n_chunks ? min(g.first_utt[cw1] + 1u, g.n_utt) : 0u;
-    const bool staged = U1 - U0 <= (uint32_t)PAIRS_UCAP;
-    uint32_t* so = s_off[wv];
-    if (staged && cw0 < g.n_chunks)
-        for (uint32_t k = lane; k <= U1 - U0; k += 64) so[k] = (uint32_t)g_off(g, U0 + k);
+    WaveRows W;
+    if (cw0 < g.n_chunks) W.stage(g, cw0, cw1, lane, s_off[wv]);
     __syncthreads();
     if (c >= g.n_chunks) return;
-    auto uoff = [&](int64_t u) { return staged ? (int64_t)so[u - U0] : g_off(g, (uint32_t)u); };
+    auto uoff = [&](int64_t u) { return W.off(g, (uint32_t)u); };
     const Lane L = g_lane(g, c);
     const uint32_t top = scan_top(g, L);
     if (top <= L.lo) return;
