@@ -1239,11 +1239,6 @@ struct EvLoc {         // where an event's candidates start (16 B: one dwordx4),
     uint32_t ustart;   // utterance start, relative to the batch base
     uint32_t uend;     // utterance end, relative to the batch base
 };
-struct EvPairs {       // an event's block of the pair queue (8 B), expanded by k_expand
-    uint32_t first;    // first pair index
-    uint16_t acc;      // D accept set
-    uint16_t n;        // pairs (patterns in the accept set)
-};
 struct PairRes {       // one (start, pattern) candidate (8 B); its FIRST end lives in pend[] (4 B)
     uint32_t ev;       // dense event index -> EvLoc
     uint16_t p;        // detector pattern
@@ -1305,7 +1300,7 @@ constexpr int PAIRS_BLOCK = 256;
 // own per-lane event list (descending position, arena g at ev + g * ev_stride), counted per group by
 // the flat pass.  The write pass (k_pairs_merge) merges the lists by position, a tie going to the
 // higher group first so that, the queue being filled back to front, group 0 (built-ins and
-// excluders) comes first among one start's pairs; k_expand then writes the pairs.  (A per-lane walk
+// excluders) comes first among one start's pairs, and writes the pairs.  (A per-lane walk
 // of the merge -- one thread per lane, two dependent global loads per event -- took 1026 us at config
 // 5; the rank form below 597 us.)
 constexpr int SCAN_GROUPS_MAX = 8;
@@ -1339,7 +1334,8 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 __device__ void merge_walk(const Geo& g, const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
                            uint32_t c, uint32_t n_groups, uint64_t ev_stride, uint32_t cnt_stride,
                            const AccTabs& acct, uint64_t top, uint64_t evb, EvLoc* __restrict__ evloc,
-                           EvPairs* __restrict__ evpairs) {
+                           const uint32_t* __restrict__ acc_off, const uint16_t* __restrict__ acc_ids,
+                           PairRes* __restrict__ pres) {
     const Lane L = g_lane(g, c);
     const uint64_t eb = ev_base(L, c);
     uint32_t gk[SCAN_GROUPS_MAX], gn[SCAN_GROUPS_MAX], hp[SCAN_GROUPS_MAX];
@@ -1389,12 +1385,15 @@ __device__ void merge_walk(const Geo& g, const Event* __restrict__ ev, const uin
         }
         const uint32_t n = npair[E.sd];
         w -= n;
-        EvPairs ep;
-        ep.first = (uint32_t)w;
-        ep.acc = accid[E.sd];
-        ep.n = (uint16_t)n;
-        evpairs[evb + k] = ep;
         if (n == 0) continue;
+        const uint32_t a0 = acc_off[accid[E.sd]];
+        for (uint32_t i = 0; i < n; ++i) {
+            PairRes P;
+            P.ev = (uint32_t)(evb + k);
+            P.p = acc_ids[a0 + i];
+            P.lik = -1;
+            pres[w + i] = P;
+        }
         EvLoc Lc;
         Lc.u = (uint32_t)u;
         Lc.s = (uint32_t)pos;
@@ -1406,7 +1405,9 @@ __device__ void merge_walk(const Geo& g, const Event* __restrict__ ev, const uin
 
 __global__ __launch_bounds__(MERGE_WAVES * 64) void k_pairs_merge(const Geo g, const Event* __restrict__ ev,
                                                            const uint32_t* __restrict__ lane_cnt,
-                                                           EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
+                                                           EvLoc* __restrict__ evloc, PairRes* __restrict__ pres,
+                                                           const uint32_t* __restrict__ acc_off,
+                                                           const uint16_t* __restrict__ acc_ids,
                                                            uint64_t pair_cap, uint64_t ev_cap,
                                                            const uint64_t* __restrict__ lane_pair,
                                                            const uint64_t* __restrict__ lane_ev,
@@ -1475,7 +1476,8 @@ __global__ __launch_bounds__(MERGE_WAVES * 64) void k_pairs_merge(const Geo g, c
     }
     if (T == 0) return;
     if (T > evw_cap) {                                // too many events to stage: walk them
-        if (own && tot) merge_walk(g, ev, lane_cnt, c, n_groups, ev_stride, cnt_stride, acct, top, evb, evloc, evpairs);
+        if (own && tot) merge_walk(g, ev, lane_cnt, c, n_groups, ev_stride, cnt_stride, acct, top, evb, evloc, acc_off,
+                                     acc_ids, pres);
         return;
     }
     if (lane == 0) lbf[SCAN_GROUPS_MAX * MERGE_LPW] = T;
@@ -1545,8 +1547,11 @@ __global__ __launch_bounds__(MERGE_WAVES * 64) void k_pairs_merge(const Geo g, c
             }
         }
     wave_lds_sync();
-    // every event's merged rank and first pair, flattened over the lists.  (Permuting the records
-    // through LDS so that the stores land in slot order measured slower: 597 -> 617 us at config 5.)
+    // every event's merged rank and first pair, flattened over the lists; then the chunk's (start,
+    // pattern) pairs, wave-cooperative as in k_pairs_flat (a separate expansion kernel reading an
+    // 8-byte record per event: merge 599 + expand 115 us against 689 us fused).
+    // (Permuting the event records through LDS so that their stores land in slot order measured
+    // slower: 597 -> 617 us at config 5.)
     for (uint32_t f0 = 0; f0 < T; f0 += 64) {
         const uint32_t f = f0 + lane;
         const bool act = f < T;
@@ -1554,42 +1559,66 @@ __global__ __launch_bounds__(MERGE_WAVES * 64) void k_pairs_merge(const Geo g, c
         const uint32_t q = li / MERGE_LPW, ow = li % MERGE_LPW;
         const uint64_t o_top = __shfl(top, (int)ow), o_evb = __shfl(evb, (int)ow);
         const uint32_t o_u0 = __shfl(u0, (int)ow), o_u1 = __shfl(u1, (int)ow);
-        if (!act) continue;
-        const uint32_t pos = sp[f], na = sa[f];
-        uint32_t k = f - lbf[li];                          // index in its own list
-        uint32_t pn = sn[f];                               // pairs up to and including it, own list
-        for (uint32_t q2 = 0; q2 < n_groups; ++q2) {       // events of q2 placed before this one
-            if (q2 == q) continue;
-            const uint32_t b2 = lbf[q2 * MERGE_LPW + ow];
-            uint32_t lo = 0, hi = lbf[q2 * MERGE_LPW + ow + 1] - b2;
-            while (lo < hi) {
-                const uint32_t m = (lo + hi) >> 1;
-                const uint32_t p2 = sp[b2 + m];
-                if (p2 > pos || (p2 == pos && q2 > q)) lo = m + 1;
-                else hi = m;
+        uint32_t n = 0, first = 0, a0 = 0, evi = 0;
+        if (act) {
+            const uint32_t pos = sp[f], na = sa[f];
+            uint32_t k = f - lbf[li];                      // index in its own list
+            uint32_t pn = sn[f];                           // pairs up to and including it, own list
+            for (uint32_t q2 = 0; q2 < n_groups; ++q2) {   // events of q2 placed before this one
+                if (q2 == q) continue;
+                const uint32_t b2 = lbf[q2 * MERGE_LPW + ow];
+                uint32_t lo = 0, hi = lbf[q2 * MERGE_LPW + ow + 1] - b2;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    const uint32_t p2 = sp[b2 + m];
+                    if (p2 > pos || (p2 == pos && q2 > q)) lo = m + 1;
+                    else hi = m;
+                }
+                k += lo;
+                if (lo) pn += sn[b2 + lo - 1];
             }
-            k += lo;
-            if (lo) pn += sn[b2 + lo - 1];
+            n = na & 0xffffu;
+            first = (uint32_t)(o_top - pn);
+            evi = (uint32_t)(o_evb + k);
+            if (n) {
+                a0 = acc_off[na >> 16];
+                uint32_t lo = o_u0, hi = o_u1 - 1;       // the event's row: last u with start <= pos
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi + 1) >> 1;
+                    if (uoff(m) <= pos) lo = m;
+                    else hi = m - 1;
+                }
+                EvLoc Lc;
+                Lc.u = lo;
+                Lc.s = pos;
+                Lc.ustart = uoff(lo);
+                Lc.uend = uoff(lo + 1);
+                evloc[evi] = Lc;
+            }
         }
-        const uint32_t n = na & 0xffffu;
-        EvPairs ep;
-        ep.first = (uint32_t)(o_top - pn);
-        ep.acc = (uint16_t)(na >> 16);
-        ep.n = (uint16_t)n;
-        evpairs[o_evb + k] = ep;
-        if (n) {
-            uint32_t lo = o_u0, hi = o_u1 - 1;           // the event's row: last u with start <= pos
-            while (lo < hi) {
-                const uint32_t m = (lo + hi + 1) >> 1;
-                if (uoff(m) <= pos) lo = m;
-                else hi = m - 1;
+        uint32_t ein = n;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(ein, d);
+            if (lane >= d) ein += o;
+        }
+        const uint32_t etot = __shfl(ein, 63);
+        for (uint32_t p0 = 0; p0 < etot; p0 += 64) {
+            const uint32_t pq = p0 + lane;
+            int lo = 0;                                   // the pair's event: first lane with ein > pq
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if (__shfl(ein, lo + st - 1) <= pq) lo += st;
+            const uint32_t p_incl = __shfl(ein, lo), p_n = __shfl(n, lo);
+            const uint32_t p_first = __shfl(first, lo), p_a0 = __shfl(a0, lo), p_ev = __shfl(evi, lo);
+            if (pq < etot) {
+                const uint32_t i = pq - (p_incl - p_n);
+                PairRes P;
+                P.ev = p_ev;
+                P.p = acc_ids[p_a0 + i];
+                P.lik = -1;
+                pres[p_first + i] = P;
             }
-            EvLoc Lc;
-            Lc.u = lo;
-            Lc.s = pos;
-            Lc.ustart = uoff(lo);
-            Lc.uend = uoff(lo + 1);
-            evloc[o_evb + k] = Lc;
         }
     }
 }
@@ -1607,7 +1636,7 @@ template <bool WRITE>
 __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, const Geo g,
                                                     const Event* __restrict__ ev, const uint32_t* __restrict__ lane_cnt,
                                                     const uint8_t* __restrict__ role, int32_t* __restrict__ kw,
-                                                    EvLoc* __restrict__ evloc, EvPairs* __restrict__ evpairs,
+                                                    EvLoc* __restrict__ evloc,
                                                     uint64_t pair_cap, uint64_t ev_cap,
                                                     const uint64_t* __restrict__ lane_pair,
                                                     const uint64_t* __restrict__ lane_ev,
@@ -1801,61 +1830,6 @@ __global__ __launch_bounds__(PAIRS_BLOCK) void k_pairs_flat(const RulesDev R, co
     if (!WRITE && valid) {
         if (n_groups > 1) atomicAdd(lane_np + c, run);
         else lane_np[c] = run;
-    }
-}
-
-// one thread per event: its (start, pattern) pairs, accept-set order (excluders first)
-__global__ __launch_bounds__(256) void k_expand(const RulesDev R, const EvPairs* __restrict__ evpairs,
-                                                const uint64_t* __restrict__ ev_count, const uint32_t* __restrict__ err,
-                                                PairRes* __restrict__ pres) {
-    __shared__ uint32_t s_off[257];
-    if (*err & ERR_ABORT) return;           // a queue overflowed: records are incomplete, the batch re-runs
-    __shared__ uint16_t s_ids[2048];
-    const uint32_t n_dacc = R.n_dacc;
-    const bool small = n_dacc < 256 && R.d_acc_off[n_dacc] <= 2048;
-    if (small) {
-        for (uint32_t i = threadIdx.x; i <= n_dacc; i += blockDim.x) s_off[i] = R.d_acc_off[i];
-        for (uint32_t i = threadIdx.x; i < R.d_acc_off[n_dacc]; i += blockDim.x) s_ids[i] = R.d_acc_ids[i];
-    }
-    __syncthreads();
-    const uint64_t n = *ev_count;
-    // wave-cooperative: the pairs of the wavefront's 64 events are numbered 0..total-1 by an inclusive
-    // scan of the counts, and lane f writes pair f, f + 64, ... (its event found by a 6-step search of
-    // the scan), so a store instruction writes 64 neighbouring records instead of record i of 64 events
-    const int lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t kb = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); kb < n; kb += stride) {
-        const uint64_t k = kb + lane;
-        EvPairs ep{0, 0, 0};
-        if (k < n) ep = evpairs[k];
-        const uint32_t a0 = ep.n == 0 ? 0u : (small ? s_off[ep.acc] : R.d_acc_off[ep.acc]);
-        uint32_t incl = ep.n;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(incl, d);
-            if (lane >= d) incl += o;
-        }
-        const uint32_t total = __shfl(incl, 63);
-        for (uint32_t f0 = 0; f0 < total; f0 += 64) {
-            const uint32_t f = f0 + lane;
-            // owner: the first lane whose inclusive count exceeds f
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-                const uint32_t v = __shfl(incl, lo + step - 1);
-                if (v <= f) lo += step;
-            }
-            const uint32_t o_incl = __shfl(incl, lo), o_n = __shfl((uint32_t)ep.n, lo);
-            const uint32_t o_a0 = __shfl(a0, lo), o_first = __shfl(ep.first, lo);
-            if (f < total) {
-                const uint32_t i = f - (o_incl - o_n);
-                PairRes P;
-                P.ev = (uint32_t)(kb + lo);
-                P.p = small ? s_ids[o_a0 + i] : R.d_acc_ids[o_a0 + i];
-                P.lik = -1;
-                pres[o_first + i] = P;
-            }
-        }
     }
 }
 
@@ -4289,7 +4263,6 @@ struct pii_engine {
     uint32_t* lane_cnt = nullptr;
     uint64_t* bnd = nullptr;
     EvLoc* evloc = nullptr;
-    EvPairs* evpairs = nullptr;
     uint64_t ev_cap = 0;
     uint64_t* lane_ev = nullptr;      // exclusive scan of lane_cnt: first dense event index per lane
     PairRes* pres = nullptr;
@@ -4605,7 +4578,7 @@ int ensure_queues(pii_engine* e, uint64_t total_bytes) {
     }
     if (e->ev_cap < total_bytes / 16 + 4096) {
         const uint64_t cap = total_bytes / 16 + 4096;
-        if ((rc = grow(e, e->evloc, cap)) || (rc = grow(e, e->evpairs, cap))) return rc;
+        if ((rc = grow(e, e->evloc, cap))) return rc;
         e->ev_cap = cap;
     }
     return PII_OK;
@@ -4703,7 +4676,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             const uint64_t es = e->cap_ev;
             if (multi) HIPCHK(hipMemsetAsync(e->lane_np, 0, (size_t)n_chunks * sizeof(uint32_t), st));
             k_pairs_flat<false><<<dim3(nbp, ns), PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                       e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                       e->pair_cap, e->ev_cap, e->lane_pair,
                                                                        e->lane_ev, e->lane_np, e->d_err, e->pres, e->acct,
                                                                        ns, es, cs, e->lane_evn);
             int rc;
@@ -4716,12 +4689,11 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             } else if (multi) {
                 const uint32_t lpb = MERGE_WAVES * MERGE_LPW;
                 k_pairs_merge<<<(n_chunks + lpb - 1) / lpb, MERGE_WAVES * 64, 0, st>>>(
-                    g, e->ev, e->lane_cnt, e->evloc, e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair, e->lane_ev,
-                    e->lane_np, e->d_err, ns, es, cs, e->acct, e->merge_cap);
-                k_expand<<<e->n_cu * 8, 256, 0, st>>>(R, e->evpairs, e->lane_ev + n_chunks, e->d_err, e->pres);
+                    g, e->ev, e->lane_cnt, e->evloc, e->pres, R.d_acc_off, R.d_acc_ids, e->pair_cap, e->ev_cap,
+                    e->lane_pair, e->lane_ev, e->lane_np, e->d_err, ns, es, cs, e->acct, e->merge_cap);
             } else {
                 k_pairs_flat<true><<<nbp, PAIRS_BLOCK, 0, st>>>(R, g, e->ev, e->lane_cnt, role, e->kw, e->evloc,
-                                                                e->evpairs, e->pair_cap, e->ev_cap, e->lane_pair,
+                                                                e->pair_cap, e->ev_cap, e->lane_pair,
                                                                 e->lane_ev, e->lane_np, e->d_err, e->pres, e->acct,
                                                                 1, 0, 0, nullptr);
             }
@@ -5565,6 +5537,9 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         // k_pair_first: two 1024-thread workgroups per CU, one round (2 or 4 rounds: 160 -> 165 / 164 µs,
         // and k_pair_eval slower on the smaller segments)
         e->n_seg = 2 * (uint32_t)e->n_cu;
+        // k_pair_eval work units per k_pair_first workgroup: 2 (config 2: 1 / 2 / 3 / 4 -> 342 / 312 / 315
+        // / 318 us); 4 when the rule lists stay in L2 (config 5's longer evaluations: 2 -> 4: 918 -> 898 us)
+        if (e->img_eval_rg.d) e->eval_split = 4;
         if (const char* v = std::getenv("PII_EVAL_SPLIT")) e->eval_split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
         if (const char* v = std::getenv("PII_MERGE_CAP")) e->merge_cap = (uint32_t)std::max(0, std::min(MERGE_EVW, std::atoi(v)));
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
@@ -5648,7 +5623,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->evpairs, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_first_hot.d, e->img_eval.d, e->img_eval_rg.d, e->img_sel.d, e->img_sel_rg.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
@@ -5747,9 +5722,7 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         // is idempotent)
         const uint64_t need = e->h_totals[3] + 4096, need_ev = e->h_totals[4] + 4096, need_wf = e->h_totals[5] + 4096;
         if (need_ev > e->ev_cap) {
-            int rc = grow(e, e->evloc, need_ev);
-            if (!rc) rc = grow(e, e->evpairs, need_ev);
-            if (rc) return rc;
+            if (int rc = grow(e, e->evloc, need_ev)) return rc;
             e->ev_cap = need_ev;
         }
         int rc = grow_pairs(e, std::max(need, e->pair_cap));

@@ -37,7 +37,7 @@ CALIB_KERNELS = {"lane_rev": "k_lane_rev", "stream16": "k_coalesced", "stream8":
 # dominant read stream per engine kernel (name prefix); anything else: stream8
 KERNEL_PATTERN = {"k_scan": "lane_rev", "k_scan_fix": "lane_rev", "k_redact": "stream16", "k_win_redact": "stream16",
                   "k_win_join": "stream16", "k_lane_bits": "stream8", "k_chunk_index": "stream8",
-                  "k_pairs_flat": "stream8", "k_pairs": "stream8", "k_expand": "stream8", "k_pair_first": "stream8",
+                  "k_pairs_flat": "stream8", "k_pairs_merge": "stream8", "k_pair_first": "stream8",
                   "k_pair_eval": "stream8", "k_select": "stream8", "k_spans": "stream8", "k_ctx_scan": "stream4",
                   "k_ctx_apply": "stream4", "k_ctx_commit": "stream4", "k_lane_count": "stream4",
                   "k_lane_place": "stream4", "k_scan_reduce": "stream4", "k_scan_apply": "stream4",
