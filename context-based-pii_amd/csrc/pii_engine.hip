@@ -1884,7 +1884,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
     }
     // a pattern's automaton: the LDS copy for the leading patterns (GI), else the image's
     auto tabs = [&](uint32_t p, Pool& pl, const int32_t*& d) {
-        const bool h = GI && p < p_hot;
+        const bool h = GI && p < p_hot && hdesc[8 * p + 3] != 0;
         pl = h ? hpool : pool;
         d = (h ? hdesc : fdesc) + 8 * p;
     };
@@ -4189,7 +4189,11 @@ bool parse_blob(const uint8_t* p, size_t n, std::vector<Section>& out) {
 
 // ================================================================================ engine object
 constexpr size_t IMG_LDS_MAX = 160 * 1024;
-constexpr size_t FIRST_HOT_LDS = 78 * 1024;     // k_pair_first<true>'s LDS copy (two 1024-thread workgroups per CU)
+// k_pair_first<true>'s LDS copy: most of the LDS, one 1024-thread workgroup per CU (config 5: 40 / 78 /
+// 156 KB -> 999 / 934 / 885 us: more automata in LDS beat two workgroups per CU)
+constexpr size_t FIRST_HOT_LDS = 156 * 1024;
+constexpr size_t FIRST_HOT_BIG = 8 * 1024;      // ... which skips automata larger than this (prefix of
+                                                // ids, 78 KB: 982 -> 933 us)
 constexpr size_t IMG_LDS_SPLIT = 80 * 1024;    // pair-kernel image size past which its per-(variant, type) lists stay in L2
 struct DevImage {
     LdsImage li{};
@@ -5467,23 +5471,47 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
             return fail("rule table upload failed");
         if (e->img_first.global) {
-            // the leading patterns' FIRST automata (built-in types first) that fit the LDS of two
-            // k_pair_first workgroups per CU, for k_pair_first<true>
+            // FIRST automata for k_pair_first<true>'s LDS copy: patterns in id
+            // order (the built-in types first), skipping any automaton over FIRST_HOT_BIG bytes, until
+            // the copy is full.  A skipped pattern keeps a descriptor with no columns (read from L2).
+            size_t big = FIRST_HOT_BIG, budget = FIRST_HOT_LDS;
+            if (const char* v = std::getenv("PII_FIRST_HOT_BIG")) big = (size_t)std::max(0, std::atoi(v));
+            if (const char* v = std::getenv("PII_FIRST_HOT_LDS"))
+                budget = std::min<size_t>(158 * 1024, (size_t)std::max(0, std::atoi(v)));
+            uint32_t cap_p = (uint32_t)R.P;
+            if (const char* v = std::getenv("PII_FIRST_HOT")) cap_p = std::min<uint32_t>(cap_p, (uint32_t)std::max(0, std::atoi(v)));
             DfaPool hf;
             uint32_t ph = 0;
-            for (int p = 0; p < R.P; ++p) {
+            size_t trans_n = 0, cmap_n = 0;
+            for (uint32_t p = 0; p < cap_p; ++p) {
                 const int32_t* d = fdesc + 8 * p;
-                const size_t tr = hf.trans.size() + 64 + (size_t)d[7] * d[3];
-                const size_t bytes = ((tr * 2 + 15) & ~(size_t)15) + ((hf.cmap.size() + 260 + 15) & ~(size_t)15) +
-                                     (((hf.desc.size() + 8) * 4 + 15) & ~(size_t)15);
-                if (bytes > FIRST_HOT_LDS) break;
-                add_dfa(hf, d, ptrans, pflags, pcmap);
-                ph = (uint32_t)p + 1;
+                const size_t dfa = (size_t)d[7] * d[3] * 2;
+                const size_t tr = trans_n + 64 + (size_t)d[7] * d[3];
+                const size_t bytes = ((tr * 2 + 15) & ~(size_t)15) + ((cmap_n + 260 + 15) & ~(size_t)15) +
+                                     (((size_t)(p + 1) * 32 + 15) & ~(size_t)15);
+                if (bytes > budget) {
+                    if (big == 0) break;
+                    continue;
+                }
+                if (big && dfa > big) continue;
+                trans_n = tr;
+                cmap_n += 260;
+                ph = p + 1;
             }
-            if (const char* v = std::getenv("PII_FIRST_HOT")) ph = std::min<uint32_t>(ph, (uint32_t)std::max(0, std::atoi(v)));
             if (ph > 0) {
-                hf = DfaPool{};
-                for (uint32_t p = 0; p < ph; ++p) add_dfa(hf, fdesc + 8 * p, ptrans, pflags, pcmap);
+                trans_n = 0;
+                for (uint32_t p = 0; p < ph; ++p) {
+                    const int32_t* d = fdesc + 8 * p;
+                    const size_t dfa = (size_t)d[7] * d[3] * 2;
+                    const size_t tr = hf.trans.size() + 64 + (size_t)d[7] * d[3];
+                    const size_t bytes = ((tr * 2 + 15) & ~(size_t)15) + ((hf.cmap.size() + 260 + 15) & ~(size_t)15) +
+                                         (((size_t)ph * 32 + 15) & ~(size_t)15);
+                    if ((big && dfa > big) || bytes > budget) {
+                        hf.desc.insert(hf.desc.end(), 8, 0);          // columns 0: not resident
+                        continue;
+                    }
+                    add_dfa(hf, d, ptrans, pflags, pcmap);
+                }
                 std::vector<std::pair<const void*, size_t>> ph_parts(FI_N);
                 ph_parts[FI_TRANS] = vec(hf.trans);
                 ph_parts[FI_CMAP] = vec(hf.cmap);
