@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -1251,13 +1252,32 @@ constexpr int IMG_MAX = 16;
 struct LdsImage {
     uint32_t off[IMG_MAX];
     uint32_t total;    // bytes, multiple of 16
+    uint32_t aux;      // index widths of the image's list tables (list_range): rule lists | exclusion lists << 3
 };
+// Per-(variant, type) hotword-rule and exclusion lists, deduplicated: key i -> list L = ix[i] (an index
+// `w` bytes wide; w = 0: L = i, the undeduplicated global tables) -> ids[loff[L], loff[L + 1]).  Config 5
+// has 23349 keys but 29 distinct rule lists and 2 exclusion lists: one byte per key instead of four,
+// so the pair kernels' images keep their lists in LDS.
+// (CL = false: the kernel instantiation for undeduplicated tables, the index not even tested -- the
+// runtime test alone cost config 2's k_select 4 us)
+template <bool CL>
+__device__ __forceinline__ void list_range(const void* ix, uint32_t w, const uint32_t* loff, uint32_t i, uint32_t& r0,
+                                           uint32_t& r1) {
+    uint32_t L = i;
+    if (CL) {
+        if (w == 1) L = static_cast<const uint8_t*>(ix)[i];
+        else if (w == 2) L = static_cast<const uint16_t*>(ix)[i];
+        else if (w == 4) L = static_cast<const uint32_t*>(ix)[i];
+    }
+    r0 = loff[L];
+    r1 = loff[L + 1];
+}
 enum { FI_TRANS, FI_CMAP, FI_DESC, FI_N };
-enum { EV_TRANS, EV_CMAP, EV_HDESC, EV_HRULE, EV_DTYPE, EV_DVAL, EV_DLIK, EV_ROFF, EV_RIDS, EV_THOT, EV_N };
+enum { EV_TRANS, EV_CMAP, EV_HDESC, EV_HRULE, EV_DTYPE, EV_DVAL, EV_DLIK, EV_ROFF, EV_RIDS, EV_THOT, EV_RLOFF, EV_N };
 // k_win_select: everything k_select reads + the HOT automata and the variants' hotword rule lists
 enum { WS_TRANS, WS_CMAP, WS_HDESC, WS_HRULE, WS_DTYPE, WS_DLIK, WS_VEN, WS_VMIN, WS_DEX, WS_XOFF, WS_XIDS,
-       WS_TOKOFF, WS_ROFF, WS_RIDS, WS_N };
-enum { SE_DTYPE, SE_VEN, SE_VMIN, SE_DEX, SE_XOFF, SE_XIDS, SE_TOKOFF, SE_N };
+       WS_TOKOFF, WS_ROFF, WS_RIDS, WS_RLOFF, WS_XLOFF, WS_N };
+enum { SE_DTYPE, SE_VEN, SE_VMIN, SE_DEX, SE_XOFF, SE_XIDS, SE_TOKOFF, SE_XLOFF, SE_N };
 
 constexpr int PAIR_BLOCK = 1024;
 
@@ -1968,7 +1988,9 @@ struct EvalTabs {
     const uint16_t* dtype;
     const uint8_t* dval;
     const uint8_t* dlik;
-    const uint32_t* roff;
+    const void* rix;          // rule lists (list_range)
+    uint32_t rw;
+    const uint32_t* rloff;
     const uint16_t* rids;
 };
 __device__ __forceinline__ EvalTabs eval_tabs(const uint8_t* lb, const LdsImage& li) {
@@ -1979,7 +2001,9 @@ __device__ __forceinline__ EvalTabs eval_tabs(const uint8_t* lb, const LdsImage&
     E.dtype = reinterpret_cast<const uint16_t*>(lb + li.off[EV_DTYPE]);
     E.dval = lb + li.off[EV_DVAL];
     E.dlik = lb + li.off[EV_DLIK];
-    E.roff = reinterpret_cast<const uint32_t*>(lb + li.off[EV_ROFF]);
+    E.rix = lb + li.off[EV_ROFF];
+    E.rw = li.aux & 7u;
+    E.rloff = reinterpret_cast<const uint32_t*>(lb + li.off[EV_RLOFF]);
     E.rids = reinterpret_cast<const uint16_t*>(lb + li.off[EV_RIDS]);
     return E;
 }
@@ -1987,12 +2011,14 @@ __device__ __forceinline__ EvalTabs eval_tabs(const uint8_t* lb, const LdsImage&
 // likelihood of the match [s, e) of pattern p in row t0[0, L) under context variant v: the validator,
 // then every hotword rule of (v, type) in order (window_before / window_after, fixed / relative); -1
 // when the validator rejects it
+template <bool CL>
 __device__ __forceinline__ int pair_lik(const EvalTabs& E, int T, const uint8_t* t0, int L, int s, int e, int p,
                                         int v) {
     if (!validate(E.dval[p], t0 + s, e - s)) return -1;
     const int t = E.dtype[p];
     int lik = E.dlik[p];
-    const uint32_t r0 = E.roff[v * T + t], r1 = E.roff[v * T + t + 1];
+    uint32_t r0, r1;
+    list_range<CL>(E.rix, E.rw, E.rloff, (uint32_t)(v * T + t), r0, r1);
     for (uint32_t q = r0; q < r1; ++q) {
         const int h = E.rids[q];
         const int wb = E.hrule[4 * h], wa = E.hrule[4 * h + 1];
@@ -2023,7 +2049,7 @@ __device__ __forceinline__ int pair_lik(const EvalTabs& E, int T, const uint8_t*
 // per matched pair: validator + hotword windows of the row's context variant -> likelihood
 // RG: the image omits the per-(variant, type) rule lists (config 5's are 107 KB: with them the image
 // leaves room for one 1024-thread workgroup per CU); they are read from global memory (L2) instead
-template <bool GI, bool RG = false>
+template <bool GI, bool RG = false, bool CL = false>
 __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_eval(const uint4* __restrict__ img, const LdsImage li, int T,
                                                           const uint8_t* __restrict__ text0,
                                                           const uint64_t* __restrict__ offs,
@@ -2041,7 +2067,9 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     EvalTabs E = eval_tabs(lb, li);
     if (RG) {
-        E.roff = g_roff;
+        E.rix = nullptr;
+        E.rw = 0;
+        E.rloff = g_roff;
         E.rids = g_rids;
     }
     const uint8_t* text = text0 + offs[0];
@@ -2075,7 +2103,7 @@ __global__ __launch_bounds__(PAIR_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8
             const int s = (int)(Lc.s - Lc.ustart), e = pend[i];
             const uint32_t u = Lc.u;
             const int v = (role[u] == PII_ROLE_CUSTOMER && ctx[u] >= 0) ? ctx[u] + 1 : 0;
-            const int lik = pair_lik(E, T, t0, L, s, e, P.p, v);
+            const int lik = pair_lik<CL>(E, T, t0, L, s, e, P.p, v);
             SelRec r;
             r.u = Lc.u;
             r.ps = s;
@@ -2126,7 +2154,9 @@ struct SelTabs {
     const uint8_t* ven;
     const uint8_t* vmin;
     const uint8_t* dex;
-    const uint32_t* xoff;
+    const void* xix;          // exclusion lists (list_range)
+    uint32_t xw;
+    const uint32_t* xloff;
     const uint16_t* xids;
     const uint32_t* tokoff;
 };
@@ -2166,7 +2196,9 @@ __device__ __forceinline__ SelTabs sel_tabs(const uint8_t* lb, const LdsImage& l
     T.ven = lb + li.off[SE_VEN];
     T.vmin = lb + li.off[SE_VMIN];
     T.dex = lb + li.off[SE_DEX];
-    T.xoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_XOFF]);
+    T.xix = lb + li.off[SE_XOFF];
+    T.xw = (li.aux >> 3) & 7u;
+    T.xloff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_XLOFF]);
     T.xids = reinterpret_cast<const uint16_t*>(lb + li.off[SE_XIDS]);
     T.tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[SE_TOKOFF]);
     return T;
@@ -2295,8 +2327,10 @@ struct LaneSel {
         if (Lg.chi && u == Lg.u1 - 1) reach = max(reach, (uint32_t)e);
     }
     // a valid candidate of type t (excluder slot xi, 0xff: none) competes for its start
+    template <bool CL>
     __device__ __forceinline__ void consider(const SelTabs& Tb, int T, int t, int lik, int e, int xi) {
-        const uint32_t x0 = Tb.xoff[v * T + t], x1 = Tb.xoff[v * T + t + 1];
+        uint32_t x0, x1;
+        list_range<CL>(Tb.xix, Tb.xw, Tb.xloff, (uint32_t)(v * T + t), x0, x1);
         bool excluded = false;
         for (uint32_t q = x0; q < x1; ++q) {
             const int xt = Tb.xids[q];
@@ -2315,6 +2349,7 @@ struct LaneSel {
         }
     }
     // a matched pair: row pu, start ps (row relative), pattern p, context variant pv, end e, likelihood lik
+    template <bool CL>
     __device__ __forceinline__ void pair(const SelTabs& Tb, const Geo& g, const SelIO& io, int T, uint32_t pu, int ps,
                                          int p, int pv, int e, int lik) {
         enter(Tb, g, io, pu, ps, e, pv);
@@ -2376,7 +2411,7 @@ struct LaneSel {
                 }
             ex_valid |= 1u << xi;
         }
-        consider(Tb, T, t, lik, e, xi);
+        consider<CL>(Tb, T, t, lik, e, xi);
     }
     // the end of the lane: the pending start and (unless the row continues into the next lane) the
     // utterance end; the lane's outputs
@@ -2398,7 +2433,7 @@ struct LaneSel {
 // EXT: the lanes' external candidates (SelIO::ext) are merged into the pair stream in (row, start)
 // order; they take part in overlap resolution (A.6) and min_likelihood like any finding, but not in
 // finditer skipping (they have no pattern) nor as excluders.
-template <bool EXT>
+template <bool EXT, bool CL>
 __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, const SelIO& io, uint32_t c0,
                            uint32_t c1) {
     const int T = R.T;
@@ -2451,7 +2486,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     auto ext_cand = [&]() {
         const int e = (int)X.end, t = X.info_type, lik = X.likelihood;
         S.enter(Tb, g, io, X.utt, (int)X.start, e, -1);
-        if (Tb.ven[S.v * T + t] && lik >= S.minlik) S.consider(Tb, T, t, lik, e, 0xff);
+        if (Tb.ven[S.v * T + t] && lik >= S.minlik) S.template consider<CL>(Tb, T, t, lik, e, 0xff);
         xload();
     };
     for (uint32_t lane = c0; lane <= c1; ++lane) {
@@ -2505,7 +2540,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
                 if (ok) r1 = io.sel[pbase + i1];
                 if (EXT)
                     while (xhave && (X.utt < r.u || (X.utt == r.u && (int)X.start <= r.ps))) ext_cand();
-                S.pair(Tb, g, io, T, r.u, r.ps, (int)(r.p & 0xffffu), (int)(r.p >> 16), e, r.lik);
+                S.template pair<CL>(Tb, g, io, T, r.u, r.ps, (int)(r.p & 0xffffu), (int)(r.p >> 16), e, r.lik);
             }
         }
         if (EXT)
@@ -2514,7 +2549,7 @@ __device__ void select_run(const RulesDev& R, const SelTabs& Tb, const Geo& g, c
     }
 }
 
-template <bool GI, bool EXT>
+template <bool GI, bool EXT, bool CL = false>
 __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                 const Geo g, const SelIO io, const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
@@ -2522,12 +2557,14 @@ __global__ __launch_bounds__(256) void k_select(const RulesDev R, const uint4* _
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     SelTabs Tb = sel_tabs(lb, li);
     if (io.g_xoff) {
-        Tb.xoff = io.g_xoff;
+        Tb.xix = nullptr;
+        Tb.xw = 0;
+        Tb.xloff = io.g_xoff;
         Tb.xids = io.g_xids;
     }
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= g.n_chunks) return;
-    select_run<EXT>(R, Tb, g, io, c, c);
+    select_run<EXT, CL>(R, Tb, g, io, c, c);
 }
 
 // ---- cut rows: which continuation lanes need the carried state (a match of an earlier lane of the
@@ -2583,7 +2620,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_sel_dirty(const Geo g, const uint
 }
 
 // re-run every maximal chain of dirty lanes from the clean lane before it (one thread per chain)
-template <bool GI, bool EXT>
+template <bool GI, bool EXT, bool CL = false>
 __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* __restrict__ img, const LdsImage li,
                                                  const Geo g, const SelIO io, const uint32_t* __restrict__ long_rows,
                                                  const uint32_t* __restrict__ long_count,
@@ -2599,7 +2636,9 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
     SelTabs Tb = sel_tabs(lb, li);
     if (io.g_xoff) {
-        Tb.xoff = io.g_xoff;
+        Tb.xix = nullptr;
+        Tb.xw = 0;
+        Tb.xloff = io.g_xoff;
         Tb.xids = io.g_xids;
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2621,7 +2660,7 @@ __global__ __launch_bounds__(256) void k_sel_fix(const RulesDev R, const uint4* 
                     const uint32_t j1 = s_chain[k];
                     uint32_t c = j1 + 1;
                     while (c + 1 < g.n_chunks && g_cut(g, c + 1) && dirty[c + 1]) ++c;
-                    select_run<EXT>(R, Tb, g, io, j1, c);
+                    select_run<EXT, CL>(R, Tb, g, io, j1, c);
                 }
                 n = 0;
                 __syncthreads();                          // the list is free again
@@ -3717,10 +3756,12 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
     const uint8_t* ven = lb + li.off[WS_VEN];
     const uint8_t* vmin = lb + li.off[WS_VMIN];
     const uint8_t* dex = lb + li.off[WS_DEX];
-    const uint32_t* xoff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_XOFF]);
+    const void* xix = lb + li.off[WS_XOFF];
+    const uint32_t* xloff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_XLOFF]);
     const uint16_t* xids = reinterpret_cast<const uint16_t*>(lb + li.off[WS_XIDS]);
     const uint32_t* tokoff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_TOKOFF]);
-    const uint32_t* roff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_ROFF]);
+    const void* rix = lb + li.off[WS_ROFF];
+    const uint32_t* rloff = reinterpret_cast<const uint32_t*>(lb + li.off[WS_RLOFF]);
     const uint16_t* rids = reinterpret_cast<const uint16_t*>(lb + li.off[WS_RIDS]);
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= B.n_utt) return;
@@ -3773,7 +3814,8 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
             const int t = dtype[p];
             if (!ven[v * T + t]) continue;
             int lik = dlik[p];
-            const uint32_t r0 = roff[v * T + t], r1 = roff[v * T + t + 1];
+            uint32_t r0, r1;
+            list_range<true>(rix, li.aux & 7u, rloff, (uint32_t)(v * T + t), r0, r1);
             // resident proximity bits: at the window start the clipped ones, with >= need predecessors
             // the ones over the halo; otherwise (or for rules past WHOT_BITS) re-run over the window
             const bool known = C.need == 0 || j == 0 || j >= (int)C.need;
@@ -3816,7 +3858,8 @@ __global__ __launch_bounds__(256) void k_win_select(const RulesDev R, const uint
                     }
                 ex_valid |= 1u << xi;
             }
-            const uint32_t x0 = xoff[v * T + t], x1 = xoff[v * T + t + 1];
+            uint32_t x0, x1;
+            list_range<true>(xix, (li.aux >> 3) & 7u, xloff, (uint32_t)(v * T + t), x0, x1);
             bool excluded = false;
             for (uint32_t q = x0; q < x1; ++q) {
                 const int xt = xids[q];
@@ -4202,6 +4245,47 @@ struct DevImage {
     size_t lds() const { return global ? 0 : li.total; }
 };
 
+// a per-(variant, type) list table, deduplicated for the LDS images (list_range)
+struct ListTab {
+    std::vector<uint8_t> ix;      // per key: list number, w bytes
+    std::vector<uint32_t> loff;   // per list: first id, + end
+    std::vector<uint16_t> ids;
+    uint32_t w = 1;
+};
+// (a small table stays as it is -- w = 0, ix empty: one LDS read less per lookup; config 2's list
+// lookups in k_select cost 4 us more through the index)
+constexpr size_t LIST_DEDUP_KEYS = 8192;
+static ListTab dedup_lists(const uint32_t* off, const uint16_t* ids, size_t n_keys) {
+    ListTab t;
+    if (n_keys <= LIST_DEDUP_KEYS) {
+        t.w = 0;
+        t.ix.push_back(0);
+        t.loff.assign(off, off + n_keys + 1);
+        t.ids.assign(ids, ids + off[n_keys]);
+        if (t.ids.empty()) t.ids.push_back(0);
+        return t;
+    }
+    std::map<std::vector<uint16_t>, uint32_t> uniq;
+    std::vector<uint32_t> num(n_keys);
+    t.loff.push_back(0);
+    for (size_t i = 0; i < n_keys; ++i) {
+        std::vector<uint16_t> l(ids + off[i], ids + off[i + 1]);
+        auto it = uniq.find(l);
+        if (it == uniq.end()) {
+            it = uniq.emplace(l, (uint32_t)uniq.size()).first;
+            t.ids.insert(t.ids.end(), l.begin(), l.end());
+            t.loff.push_back((uint32_t)t.ids.size());
+        }
+        num[i] = it->second;
+    }
+    const size_t n = uniq.size();
+    t.w = n <= 256 ? 1u : (n <= 65536 ? 2u : 4u);
+    t.ix.resize(n_keys * t.w);
+    for (size_t i = 0; i < n_keys; ++i) std::memcpy(t.ix.data() + i * t.w, &num[i], t.w);   // little endian
+    if (t.ids.empty()) t.ids.push_back(0);
+    return t;
+}
+
 // packs `parts` (16-byte aligned sections) into one image and uploads it
 static bool make_image(const std::vector<std::pair<const void*, size_t>>& parts, DevImage& out) {
     if (parts.size() > (size_t)IMG_MAX) return false;
@@ -4241,6 +4325,7 @@ struct pii_engine {
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
     DevImage img_first_hot;            // img_first past LDS: the automata of its first first_p_hot patterns
     uint32_t first_p_hot = 0;
+    bool lists_cl = false;             // the images' rule / exclusion lists are deduplicated (list_range)
     DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
     DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
     int n_cu = 256;
@@ -4792,7 +4877,9 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), R.rule_off,
                 R.rule_ids, e->eval_split);
         } else {
-            (e->img_eval.global ? k_pair_eval<true> : k_pair_eval<false>)<<<e->n_seg * e->eval_split, PAIR_BLOCK,
+            (e->img_eval.global ? (e->lists_cl ? k_pair_eval<true, false, true> : k_pair_eval<true>)
+                                : (e->lists_cl ? k_pair_eval<false, false, true> : k_pair_eval<false>))<<<
+                e->n_seg * e->eval_split, PAIR_BLOCK,
                                                                              e->img_eval.lds(), st>>>(
                 e->img_eval.d, e->img_eval.li, R.T, text, offs, role, ctx, pcount, e->pair_cap, e->matched,
                 e->mcount, e->n_seg, e->evloc, e->pend, e->pres, reinterpret_cast<SelRec*>(e->cont), nullptr, nullptr,
@@ -4804,10 +4891,17 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                        e->lane_nf, e->lane_rd, e->lane_reach, e->out_len, e->spill, ext, ext_n, ext_stride, e->d_err,
                        xg ? R.excl_off : nullptr, xg ? R.excl_ids : nullptr};
         const bool gi = isel.global;
-        auto ksel = has_ext ? (gi ? k_select<true, true> : k_select<false, true>)
-                            : (gi ? k_select<true, false> : k_select<false, false>);
-        auto kfix = has_ext ? (gi ? k_sel_fix<true, true> : k_sel_fix<false, true>)
-                            : (gi ? k_sel_fix<true, false> : k_sel_fix<false, false>);
+        // (CL: the images hold deduplicated exclusion lists -- a large rule set; the RG path reads the
+        // original tables from L2)
+        const bool cl = e->lists_cl && !xg;
+        auto ksel = cl ? (has_ext ? (gi ? k_select<true, true, true> : k_select<false, true, true>)
+                                  : (gi ? k_select<true, false, true> : k_select<false, false, true>))
+                       : (has_ext ? (gi ? k_select<true, true> : k_select<false, true>)
+                                  : (gi ? k_select<true, false> : k_select<false, false>));
+        auto kfix = cl ? (has_ext ? (gi ? k_sel_fix<true, true, true> : k_sel_fix<false, true, true>)
+                                  : (gi ? k_sel_fix<true, false, true> : k_sel_fix<false, false, true>))
+                       : (has_ext ? (gi ? k_sel_fix<true, true> : k_sel_fix<false, true>)
+                                  : (gi ? k_sel_fix<true, false> : k_sel_fix<false, false>));
         ksel<<<(n_chunks + 255) / 256, 256, isel.lds(), st>>>(Rsel, isel.d, isel.li, g, io, e->d_err);
         const uint32_t rg = row_grid(e, total_bytes);
         k_sel_dirty<<<rg, ROW_BLOCK, 0, st>>>(g, e->long_rows, e->long_count, e->lane_reach, e->dirty, e->d_err);
@@ -5432,8 +5526,16 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         pe[EV_DTYPE] = sec("det.type");
         pe[EV_DVAL] = sec("det.validator");
         pe[EV_DLIK] = sec("det.lik");
-        pe[EV_ROFF] = sec("var.rule_off");
-        pe[EV_RIDS] = sec("var.rule_ids");
+        const size_t n_keys = (size_t)R.V * R.T;
+        const ListTab rl = dedup_lists((const uint32_t*)find("var.rule_off")->data,
+                                       (const uint16_t*)find("var.rule_ids")->data, n_keys);
+        const ListTab xl = dedup_lists((const uint32_t*)find("var.excl_off")->data,
+                                       (const uint16_t*)find("var.excl_ids")->data, n_keys);
+        const uint32_t aux = rl.w | xl.w << 3;
+        e->lists_cl = rl.w != 0 || xl.w != 0;
+        pe[EV_ROFF] = vec(rl.ix);
+        pe[EV_RLOFF] = vec(rl.loff);
+        pe[EV_RIDS] = vec(rl.ids);
         // per type: every hotword rule it has in any context variant (k_win_eval's resident bits)
         std::vector<uint32_t> thot(std::max(R.T, 1), 0u);
         {
@@ -5455,21 +5557,27 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         pw[WS_VEN] = sec("var.enabled");
         pw[WS_VMIN] = sec("var.minlik");
         pw[WS_DEX] = sec("det.exidx");
-        pw[WS_XOFF] = sec("var.excl_off");
-        pw[WS_XIDS] = sec("var.excl_ids");
+        pw[WS_XOFF] = vec(xl.ix);
+        pw[WS_XLOFF] = vec(xl.loff);
+        pw[WS_XIDS] = vec(xl.ids);
         pw[WS_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
-        pw[WS_ROFF] = sec("var.rule_off");
-        pw[WS_RIDS] = sec("var.rule_ids");
+        pw[WS_ROFF] = vec(rl.ix);
+        pw[WS_RLOFF] = vec(rl.loff);
+        pw[WS_RIDS] = vec(rl.ids);
         if (!make_image(pw, e->img_wsel)) return fail("rule table upload failed");
+        e->img_wsel.li.aux = aux;
         ps[SE_DTYPE] = sec("det.type");
         ps[SE_VEN] = sec("var.enabled");
         ps[SE_VMIN] = sec("var.minlik");
         ps[SE_DEX] = sec("det.exidx");
-        ps[SE_XOFF] = sec("var.excl_off");
-        ps[SE_XIDS] = sec("var.excl_ids");
+        ps[SE_XOFF] = vec(xl.ix);
+        ps[SE_XLOFF] = vec(xl.loff);
+        ps[SE_XIDS] = vec(xl.ids);
         ps[SE_TOKOFF] = std::make_pair((const void*)tok_off.data(), tok_off.size() * 4);
         if (!make_image(pf, e->img_first) || !make_image(pe, e->img_eval) || !make_image(ps, e->img_sel))
             return fail("rule table upload failed");
+        e->img_eval.li.aux = aux;
+        e->img_sel.li.aux = aux;
         if (e->img_first.global) {
             // FIRST automata for k_pair_first<true>'s LDS copy: patterns in id
             // order (the built-in types first), skipping any automaton over FIRST_HOT_BIG bytes, until
@@ -5527,6 +5635,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (e->img_eval.li.total > IMG_LDS_SPLIT) {
             auto pr = pe;
             pr[EV_ROFF] = std::make_pair((const void*)nullptr, (size_t)0);
+            pr[EV_RLOFF] = std::make_pair((const void*)nullptr, (size_t)0);
             pr[EV_RIDS] = std::make_pair((const void*)nullptr, (size_t)0);
             if (!make_image(pr, e->img_eval_rg)) return fail("rule table upload failed");
             if (e->img_eval_rg.global || (e->img_eval_rg.li.total > 64 * 1024 &&
@@ -5540,6 +5649,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         if (e->img_sel.li.total > IMG_LDS_SPLIT) {
             auto pr = ps;
             pr[SE_XOFF] = std::make_pair((const void*)nullptr, (size_t)0);
+            pr[SE_XLOFF] = std::make_pair((const void*)nullptr, (size_t)0);
             pr[SE_XIDS] = std::make_pair((const void*)nullptr, (size_t)0);
             if (!make_image(pr, e->img_sel_rg)) return fail("rule table upload failed");
             if (e->img_sel_rg.global || e->img_sel_rg.li.total > 64 * 1024) {      // (no gain: keep the full image)
@@ -5552,6 +5662,10 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             {(const void*)k_pair_first<false>, &e->img_first}, {(const void*)k_pair_eval<false>, &e->img_eval},
             {(const void*)k_select<false, false>, &e->img_sel}, {(const void*)k_sel_fix<false, false>, &e->img_sel},
             {(const void*)k_select<false, true>, &e->img_sel}, {(const void*)k_sel_fix<false, true>, &e->img_sel},
+            {(const void*)k_select<false, false, true>, &e->img_sel},
+            {(const void*)k_sel_fix<false, false, true>, &e->img_sel},
+            {(const void*)k_select<false, true, true>, &e->img_sel}, {(const void*)k_sel_fix<false, true, true>, &e->img_sel},
+            {(const void*)k_pair_eval<false, false, true>, &e->img_eval},
             {(const void*)k_win_eval<false>, &e->img_eval},
             {(const void*)k_win_select<false>, &e->img_wsel}, {(const void*)k_win_halo<false>, &e->img_eval}};
         for (auto& kb : big)
@@ -5566,8 +5680,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         // and k_pair_eval slower on the smaller segments)
         e->n_seg = 2 * (uint32_t)e->n_cu;
         // k_pair_eval work units per k_pair_first workgroup: 2 (config 2: 1 / 2 / 3 / 4 -> 342 / 312 / 315
-        // / 318 us); 4 when the rule lists stay in L2 (config 5's longer evaluations: 2 -> 4: 918 -> 898 us)
-        if (e->img_eval_rg.d) e->eval_split = 4;
+        // / 318 us); 4 for a large rule set (config 5's longer evaluations: 2 -> 4: 909 -> 893 us)
+        if ((size_t)R.V * R.T > LIST_DEDUP_KEYS) e->eval_split = 4;
         if (const char* v = std::getenv("PII_EVAL_SPLIT")) e->eval_split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
         if (const char* v = std::getenv("PII_MERGE_CAP")) e->merge_cap = (uint32_t)std::max(0, std::min(MERGE_EVW, std::atoi(v)));
         if (hipMalloc(&e->mcount, e->n_seg * PAIR_WAVES * sizeof(uint32_t)) != hipSuccess) return fail("hipMalloc failed");
