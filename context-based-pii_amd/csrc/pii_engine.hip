@@ -1336,12 +1336,14 @@ struct AccTabs {                 // per SCAN group, by D transition index:
 // -- the walk above) is its index in its own list plus, per other group, a binary search of that
 // group's list in LDS; its first pair is the lane's top minus the pairs of every event up to and
 // including it.  So no lane walks a serial chain of dependent global loads.  A wavefront whose
-// lanes hold more than `evw_cap` events walks them one by one instead (merge_walk).
+// lanes hold more than `evw_cap` events walks them one by one instead (merge_walk).  Shape (config 5,
+// ~34 events per lane; lanes / staged events per wavefront -> us): 16/1024 1127, 8/512 696, 8/256 1698
+// (most wavefronts walk), 4/384 690, 4/256 588, 2/256 769, 2/128 748.
 #ifndef MERGE_LPW
-#define MERGE_LPW 8
+#define MERGE_LPW 4
 #endif
 #ifndef MERGE_EVW
-#define MERGE_EVW 512
+#define MERGE_EVW 256
 #endif
 constexpr int MERGE_WAVES = 4;
 constexpr int MERGE_UCAP = 512;      // utterances of its lanes a wavefront stages
