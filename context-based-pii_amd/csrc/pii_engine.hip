@@ -863,12 +863,22 @@ constexpr int FIX_Q = 512;
 // static LDS): queue, entry states, previous round's lanes, counters
 constexpr size_t FIX_LDS = (3 * FIX_Q + 4) * 4;
 
-__global__ __launch_bounds__(256) void k_scan_fix(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+// All SCAN groups in one launch (blockIdx.y = group, its tables and arenas; one launch instead of one
+// per group: config 5's seven idle launches cost 33 us per step).
+__global__ __launch_bounds__(256) void k_scan_fix(const RulesDev* __restrict__ Rs, const uint32_t* __restrict__ lds_of,
+                                                  const Geo g, const uint8_t* __restrict__ text,
                                                   const uint32_t* __restrict__ long_rows,
-                                                  const uint32_t* __restrict__ long_count, Event* __restrict__ ev,
-                                                  uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
-                                                  uint32_t scan_lds, uint32_t* __restrict__ err) {
+                                                  const uint32_t* __restrict__ long_count, Event* __restrict__ ev0,
+                                                  uint64_t ev_stride, uint32_t* __restrict__ cnt0,
+                                                  uint32_t* __restrict__ st0, uint64_t lane_stride,
+                                                  uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+    if (blockIdx.x >= *long_count) return;
+    const RulesDev R = Rs[blockIdx.y];
+    const uint32_t scan_lds = lds_of[blockIdx.y];
+    Event* __restrict__ ev = ev0 + blockIdx.y * ev_stride;
+    uint32_t* __restrict__ lane_cnt = cnt0 + blockIdx.y * lane_stride;
+    uint32_t* __restrict__ lane_st = st0 + 2 * blockIdx.y * lane_stride;
     uint32_t* s_q = smem32 + scan_lds / 4;
     uint32_t* s_e = s_q + FIX_Q;
     uint32_t* s_prev = s_e + FIX_Q;
@@ -4322,6 +4332,9 @@ struct pii_engine {
     uint32_t n_sg = 1;
     std::vector<RulesDev> sg;
     std::vector<size_t> sg_lds;
+    RulesDev* d_sg = nullptr;          // sg and sg_lds in device memory (k_scan_fix, all groups at once)
+    uint32_t* d_sg_lds = nullptr;
+    size_t max_sg_lds = 0;
     AccTabs acct{};
     uint32_t* lane_evn = nullptr;      // per lane: events of all groups (k_pairs_merge)
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
@@ -4757,10 +4770,11 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                     (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], st>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
                 if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
-                if (e->long_min != NO_CUTS)
-                    k_scan_fix<<<row_grid(e, total_bytes), 256, e->sg_lds[q] + FIX_LDS, st>>>(
-                        Rq, g, text, e->long_rows, e->long_count, evq, cq, stq, (uint32_t)e->sg_lds[q], e->d_err);
             }
+            if (e->long_min != NO_CUTS)
+                k_scan_fix<<<dim3(row_grid(e, total_bytes), e->n_sg), 256, e->max_sg_lds + FIX_LDS, st>>>(
+                    e->d_sg, e->d_sg_lds, g, text, e->long_rows, e->long_count, e->ev, e->cap_ev, e->lane_cnt,
+                    e->lane_st, e->cap_lanes, e->d_err);
             const uint32_t nbp = (n_chunks + PAIRS_BLOCK - 1) / PAIRS_BLOCK;
             const bool multi = e->n_sg > 1;
             const uint32_t ns = e->n_sg, cs = (uint32_t)e->cap_lanes;
@@ -5719,6 +5733,15 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
         e->acct.npair[q + 1] = Rq.d_npair;
     }
     const size_t max_lds = *std::max_element(e->sg_lds.begin(), e->sg_lds.end());
+    e->max_sg_lds = max_lds;
+    {
+        std::vector<uint32_t> lds32(e->sg_lds.begin(), e->sg_lds.end());
+        if (hipMalloc(&e->d_sg, e->sg.size() * sizeof(RulesDev)) != hipSuccess ||
+            hipMalloc(&e->d_sg_lds, lds32.size() * 4) != hipSuccess ||
+            hipMemcpy(e->d_sg, e->sg.data(), e->sg.size() * sizeof(RulesDev), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(e->d_sg_lds, lds32.data(), lds32.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return fail("hipMalloc failed");
+    }
     if (max_lds > 64 * 1024 &&
         (hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
@@ -5775,7 +5798,7 @@ int pii_engine_destroy(pii_engine* e) {
                     e->wc_n, e->wbound, e->n_wfind, e->wout_len, e->wfbase, e->wspan_offs, e->wnew, e->wctx, e->wfd,
                     e->long_rows, e->lane_st, e->lane_geo, e->lane_evn, e->lane_nf, e->lane_rd, e->lane_reach, e->lane_rowbase,
                     e->dirty, e->lane_sp, e->spill, e->rsp, e->tile_first, e->h_ext, e->h_ext_n, e->jbuf, e->joff,
-                    e->jlen, e->kw2, e->jrole, e->err_saved};
+                    e->jlen, e->kw2, e->jrole, e->err_saved, e->d_sg, e->d_sg_lds};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->h_totals) (void)hipHostFree(e->h_totals);
