@@ -4340,7 +4340,9 @@ struct pii_engine {
     DevImage img_first, img_eval, img_sel, img_wsel;     // per-kernel LDS images of the rule tables
     DevImage img_first_hot;            // img_first past LDS: the automata of its first first_p_hot patterns
     uint32_t first_p_hot = 0;
-    bool lists_cl = false;             // the images' rule / exclusion lists are deduplicated (list_range)
+    bool lists_cl = false;
+    hipStream_t aux = nullptr;         // second stream for the odd SCAN groups' passes (PII_SCAN_STREAMS=1: off)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;             // the images' rule / exclusion lists are deduplicated (list_range)
     DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
     DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
     int n_cu = 256;
@@ -4750,7 +4752,10 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_lane_count<<<nsb, 256, 0, st>>>(g0, e->lane_bkt, e->lane_geo);
             k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
             // one pass per SCAN group (one for the shipped rules): halo states, scan, stitching; the
-            // utterance-start words are written once
+            // utterance-start words are written once.  Several groups: the odd ones on a second stream
+            // (forked after the words, joined before the pairs), so one pass's tail -- the last
+            // workgroups of its longest-first lanes -- overlaps the next pass.
+            const bool two = e->n_sg > 1 && e->aux != nullptr;
             for (uint32_t q = 0; q < e->n_sg; ++q) {
                 const RulesDev& Rq = e->sg[q];
                 Event* evq = e->ev + (uint64_t)q * e->cap_ev;
@@ -4760,17 +4765,28 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 if (!SCAN_INLINE_HALO && e->long_min != NO_CUTS)
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
-                if (q == 0) HIPCHK(hipEventRecord(e->kev[0], st));
+                if (q == 0) {
+                    HIPCHK(hipEventRecord(e->kev[0], st));
+                    if (two) {
+                        HIPCHK(hipEventRecord(e->ev_fork, st));
+                        HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+                    }
+                }
+                const hipStream_t sq = (two && (q & 1u)) ? e->aux : st;
                 // a WIDE table (row offsets / 2) that still leaves room for two workgroups per CU runs
                 // at 768 threads too: 6 waves/SIMD instead of 4 (config 5: the 262 regex types' 70 KB
                 // table); only the dictionary groups' ~100 KB tables need one 1024-thread workgroup
                 const bool one_wg = e->sg_lds[q] > SCAN_LDS_TWO_WG;
                 const int nt = one_wg ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
                 (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
-                    (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], st>>>(
+                    (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], sq>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
-                if (q + 1 == e->n_sg) HIPCHK(hipEventRecord(e->kev[1], st));
             }
+            if (two) {
+                HIPCHK(hipEventRecord(e->ev_join, e->aux));
+                HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
+            }
+            HIPCHK(hipEventRecord(e->kev[1], st));
             if (e->long_min != NO_CUTS)
                 k_scan_fix<<<dim3(row_grid(e, total_bytes), e->n_sg), 256, e->max_sg_lds + FIX_LDS, st>>>(
                     e->d_sg, e->d_sg_lds, g, text, e->long_rows, e->long_count, e->ev, e->cap_ev, e->lane_cnt,
@@ -5758,6 +5774,12 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     e->hist_types = (uint32_t)std::min(R.T, 1024);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     e->own_stream = true;
+    if (!(std::getenv("PII_SCAN_STREAMS") && std::atoi(std::getenv("PII_SCAN_STREAMS")) == 1) && e->n_sg > 1) {
+        if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
+            return fail("stream");
+    }
     for (auto& t : e->kev)
         if (hipEventCreate(&t) != hipSuccess) return fail("event");
     for (auto& t : e->tev)
@@ -5808,6 +5830,9 @@ int pii_engine_destroy(pii_engine* e) {
     for (auto& t : e->kev)
         if (t) (void)hipEventDestroy(t);
     if (e->stream && e->own_stream) (void)hipStreamDestroy(e->stream);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->aux) (void)hipStreamDestroy(e->aux);
     delete e;
     return PII_OK;
 }
