@@ -862,6 +862,10 @@ constexpr int FIX_Q = 512;
 // LDS past the scan tables (the tables' entries are absolute LDS addresses, so the kernel declares no
 // static LDS): queue, entry states, previous round's lanes, counters
 constexpr size_t FIX_LDS = (3 * FIX_Q + 4) * 4;
+#ifndef SCAN_STREAMS
+#define SCAN_STREAMS 3                // streams for several SCAN groups' passes (config 5, wall per step, one box:
+                                      // 1 / 2 / 3 -> 6.65 / 6.31 / 6.28 ms)
+#endif
 
 // All SCAN groups in one launch (blockIdx.y = group, its tables and arenas; one launch instead of one
 // per group: config 5's seven idle launches cost 33 us per step).
@@ -4341,8 +4345,9 @@ struct pii_engine {
     DevImage img_first_hot;            // img_first past LDS: the automata of its first first_p_hot patterns
     uint32_t first_p_hot = 0;
     bool lists_cl = false;
-    hipStream_t aux = nullptr;         // second stream for the odd SCAN groups' passes (PII_SCAN_STREAMS=1: off)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;             // the images' rule / exclusion lists are deduplicated (list_range)
+    hipStream_t aux[2] = {nullptr, nullptr};   // more streams for the SCAN groups' passes (PII_SCAN_STREAMS)
+    uint32_t n_aux = 0;
+    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};             // the images' rule / exclusion lists are deduplicated (list_range)
     DevImage img_eval_rg;     // k_pair_eval's image without the rule lists (built when img_eval is past IMG_LDS_SPLIT)
     DevImage img_sel_rg;      // k_select's image without the exclusion lists (likewise)
     int n_cu = 256;
@@ -4752,10 +4757,11 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_lane_count<<<nsb, 256, 0, st>>>(g0, e->lane_bkt, e->lane_geo);
             k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
             // one pass per SCAN group (one for the shipped rules): halo states, scan, stitching; the
-            // utterance-start words are written once.  Several groups: the odd ones on a second stream
-            // (forked after the words, joined before the pairs), so one pass's tail -- the last
-            // workgroups of its longest-first lanes -- overlaps the next pass.
-            const bool two = e->n_sg > 1 && e->aux != nullptr;
+            // utterance-start words are written once.  Several groups: group q on stream q mod
+            // SCAN_STREAMS (forked after the words, joined before the pairs), so one pass's tail -- the
+            // last workgroups of its longest-first lanes -- overlaps the next passes.
+            const uint32_t ns_scan = e->n_sg > 1 ? 1 + e->n_aux : 1;
+            const bool two = ns_scan > 1;
             for (uint32_t q = 0; q < e->n_sg; ++q) {
                 const RulesDev& Rq = e->sg[q];
                 Event* evq = e->ev + (uint64_t)q * e->cap_ev;
@@ -4769,10 +4775,11 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                     HIPCHK(hipEventRecord(e->kev[0], st));
                     if (two) {
                         HIPCHK(hipEventRecord(e->ev_fork, st));
-                        HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+                        for (uint32_t i = 0; i + 1 < ns_scan; ++i) HIPCHK(hipStreamWaitEvent(e->aux[i], e->ev_fork, 0));
                     }
                 }
-                const hipStream_t sq = (two && (q & 1u)) ? e->aux : st;
+                const uint32_t si = q % ns_scan;
+                const hipStream_t sq = si ? e->aux[si - 1] : st;
                 // a WIDE table (row offsets / 2) that still leaves room for two workgroups per CU runs
                 // at 768 threads too: 6 waves/SIMD instead of 4 (config 5: the 262 regex types' 70 KB
                 // table); only the dictionary groups' ~100 KB tables need one 1024-thread workgroup
@@ -4782,9 +4789,9 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                     (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], sq>>>(
                     Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
             }
-            if (two) {
-                HIPCHK(hipEventRecord(e->ev_join, e->aux));
-                HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
+            for (uint32_t i = 0; i + 1 < ns_scan; ++i) {
+                HIPCHK(hipEventRecord(e->ev_join[i], e->aux[i]));
+                HIPCHK(hipStreamWaitEvent(st, e->ev_join[i], 0));
             }
             HIPCHK(hipEventRecord(e->kev[1], st));
             if (e->long_min != NO_CUTS)
@@ -5774,11 +5781,15 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     e->hist_types = (uint32_t)std::min(R.T, 1024);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     e->own_stream = true;
-    if (!(std::getenv("PII_SCAN_STREAMS") && std::atoi(std::getenv("PII_SCAN_STREAMS")) == 1) && e->n_sg > 1) {
-        if (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
-            return fail("stream");
+    if (e->n_sg > 1) {
+        int ns_scan = SCAN_STREAMS;
+        if (const char* v = std::getenv("PII_SCAN_STREAMS")) ns_scan = std::max(1, std::min(3, std::atoi(v)));
+        e->n_aux = (uint32_t)ns_scan - 1;
+        if (e->n_aux && hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess) return fail("event");
+        for (uint32_t i = 0; i < e->n_aux; ++i)
+            if (hipStreamCreateWithFlags(&e->aux[i], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&e->ev_join[i], hipEventDisableTiming) != hipSuccess)
+                return fail("stream");
     }
     for (auto& t : e->kev)
         if (hipEventCreate(&t) != hipSuccess) return fail("event");
@@ -5831,8 +5842,10 @@ int pii_engine_destroy(pii_engine* e) {
         if (t) (void)hipEventDestroy(t);
     if (e->stream && e->own_stream) (void)hipStreamDestroy(e->stream);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->aux) (void)hipStreamDestroy(e->aux);
+    for (uint32_t i = 0; i < 2; ++i) {
+        if (e->ev_join[i]) (void)hipEventDestroy(e->ev_join[i]);
+        if (e->aux[i]) (void)hipStreamDestroy(e->aux[i]);
+    }
     delete e;
     return PII_OK;
 }
