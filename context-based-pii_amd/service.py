@@ -111,7 +111,13 @@ class SlotMap:
     free list is empty, and a failed one doubles it, so the cost per slot handed out stays O(1)
     amortised.)  When the table cannot grow -- the device has no memory for the doubled table
     (``on_grow`` raises PiiError NOMEM) or ``max_slots`` is reached -- the PiiError goes to the
-    caller, which answers that conversation's rows with the reference's error string."""
+    caller, which answers that conversation's rows with the reference's error string.  A failed
+    growth is remembered: until a slot is released or ``grow_retry_s`` has passed, the table does not
+    try to grow again (no repeated doubled allocation under the service lock), and within one
+    ``assign`` call the new conversations after the first that got no slot fail without another walk
+    (nothing in that call can free a slot)."""
+
+    grow_retry_s = 1.0
 
     def __init__(self, n_slots: int, on_evict: Optional[Callable[[int], None]] = None,
                  on_grow: Optional[Callable[[int], None]] = None, max_slots: Optional[int] = None):
@@ -125,6 +131,8 @@ class SlotMap:
         self._free = list(range(n_slots - 1, 0, -1))
         self.live_until: Dict[int, int] = {}      # slot -> time its context record expires (us)
         self.windowed: set = set()                 # slots holding window history
+        self._grow_failed: Optional[Tuple[int, float, PiiError]] = None   # (n_slots, when, error)
+        self.grow_calls = 0                        # on_grow attempts (accounting / tests)
 
     @property
     def capacity(self) -> int:
@@ -189,8 +197,17 @@ class SlotMap:
         n = self.n_slots * 2
         if self.max_slots is not None and n > self.max_slots:
             raise PiiError(PII_E_NOMEM, f"conversation table at its maximum of {self.max_slots} slots")
+        f = self._grow_failed
+        if f is not None and f[0] == self.n_slots and time.monotonic() - f[1] < self.grow_retry_s:
+            raise f[2]                            # the same growth failed a moment ago: do not retry
         if self.on_grow:
-            self.on_grow(n)                       # raises PiiError if the device cannot hold the larger table
+            self.grow_calls += 1
+            try:
+                self.on_grow(n)                   # raises PiiError if the device cannot hold the larger table
+            except PiiError as e:
+                self._grow_failed = (self.n_slots, time.monotonic(), e)
+                raise
+        self._grow_failed = None
         self._free = list(range(n - 1, self.n_slots - 1, -1)) + self._free
         self.n_slots = n
 
@@ -202,7 +219,9 @@ class SlotMap:
         failed: Dict[object, int] = {}
         code = 0
         for cid in conversation_ids:
-            if cid in failed:
+            if cid in failed or (code and cid not in self._map):
+                # (a new conversation after a failure of this call: nothing since has freed a slot)
+                failed.setdefault(cid, code)
                 out.append(None)
                 continue
             try:
@@ -221,6 +240,7 @@ class SlotMap:
         if s is not None:
             self._forget(s)
             self._free.append(s)
+            self._grow_failed = None
         return s
 
 
@@ -549,6 +569,11 @@ class PiiService:
             try:
                 self._note(slots, roles, [r[2] for r in rows], ts, res.ctx_info)
             except Exception:                           # noqa: BLE001 - the call stays answered
+                # the device may hold a record for any AGENT slot of the call: mark them all live, so
+                # the slot map never reuses a slot whose context the reference would still read
+                for sl, r, t_ in zip(slots, roles, ts):
+                    if r == ROLE_AGENT:
+                        self.slots.note_context(sl, t_ + self.ttl_us)
                 logging.getLogger(__name__).exception("host context bookkeeping failed after a committed call")
             for k, (slot, i, text, role, split_last) in enumerate(rows):
                 kind, data = reqs[i]

@@ -215,6 +215,33 @@ def test_slot_map_resize_failure_reuses_any_expired_slot_then_raises():
         cap.get("z", now_us=10)
 
 
+class _WindowOracleEngine(OracleEngine):
+    """OracleEngine with the window re-scan surface (window_enable / rescan_window): each row joins
+    its slot's last window_n utterances (oracle.process_window_rows' rule)."""
+
+    def __init__(self, cfg, n_slots=8, fail_code=None):
+        super().__init__(cfg, n_slots, fail_code)
+        self.window_n = 0
+        self.hist = {}
+
+    def window_enable(self, n, slot_bytes):
+        self.window_n = n
+
+    def rescan_window(self, texts, slots, roles, ts):
+        E = pkg("engine")
+        ctx = self.context_update(texts, slots, roles, ts)
+        outs = []
+        for t, s, r, now in zip(texts, slots, roles, ts):
+            w = self.hist.setdefault(s, [])
+            w.append(t)
+            del w[:-self.window_n]
+            g, t0 = self.context_get(s)
+            et = self.group_types[g] if g >= 0 and now - t0 < 90_000_000 else None
+            outs.append(self.O.redact(b"\n".join(w), self.cfg, et)[0])
+        data, offs = E.pack(outs)
+        return E.BatchResult(data, offs, np.zeros(0, E.SPAN_DTYPE), ctx)
+
+
 class _NoGrowEngine(OracleEngine):
     def context_resize(self, n):
         E = pkg("engine")
@@ -248,6 +275,55 @@ def test_resize_failure_maps_rows_to_error_strings(oracle_cfg):
     out = svc.rescan_window_batch([{"conversation_id": "v8", "participant_role": "END_USER", "text": cust,
                                     "start_timestamp_usec": 200}]) if hasattr(svc.engine, "rescan_window") else None
     assert out in (None, [f"[DLP_PROCESSING_ERROR] {cust}"])
+
+
+def test_window_rescan_without_slots_answers_errors_and_marks_windows(oracle_cfg):
+    """the window re-scan of a run some of whose conversations get no slot (the
+    table is at max_slots) answers those rows with the reference's error string; the others are
+    re-scanned and their slots marked as holding window history (never reused while open)."""
+    from oracle import pii_oracle as O
+    S = pkg("service")
+    svc = S.PiiService(engine=_WindowOracleEngine(oracle_cfg, n_slots=4), clock=Clock(), time_base="payload",
+                       max_slots=4)
+    cust = "it is jane.doe@example.com"
+    rows = [{"conversation_id": f"w{c}", "participant_role": "END_USER", "text": cust, "start_timestamp_usec": 10}
+            for c in range(5)]
+    got = svc.rescan_window_batch(rows)
+    assert got[:3] == [O.redact(cust.encode(), oracle_cfg, None)[0].decode()] * 3
+    assert got[3:] == [f"[DLP_PROCESSING_ERROR] {cust}"] * 2
+    held = [svc.slots.peek(f"w{c}") for c in range(3)]
+    assert all(h is not None for h in held) and all(h in svc.slots.windowed for h in held)
+    assert svc.slots.peek("w3") is None and svc.slots.peek("w4") is None
+    # a second turn of a windowed conversation joins its window
+    got = svc.rescan_window_batch([{"conversation_id": "w0", "participant_role": "END_USER", "text": "ok",
+                                    "start_timestamp_usec": 20}])
+    assert got == [O.redact(b"\n".join([cust.encode(), b"ok"]), oracle_cfg, None)[0].decode()]
+
+
+def test_slot_map_growth_failure_is_not_retried_per_conversation():
+    """a failed growth is remembered -- a batch of M new conversations makes
+    one on_grow attempt (and one victim walk), not M; a released slot allows growth again."""
+    S, E = pkg("service"), pkg("engine")
+    calls = []
+
+    def no_grow(n):
+        calls.append(n)
+        raise E.PiiError(E.PII_E_NOMEM, "no memory")
+    m = S.SlotMap(8, on_grow=no_grow)
+    for k in range(m.capacity):
+        m.note_context(m.get(f"c{k}", now_us=0), 1000)        # all live
+    out, code = m.assign([f"n{k}" for k in range(50)] + ["c0"], None, 10)
+    assert code == E.PII_E_NOMEM and out[:50] == [None] * 50 and out[50] is not None
+    assert calls == [16] and m.grow_calls == 1
+    for k in range(20):                                         # later calls: no retry for a while
+        with pytest.raises(E.PiiError):
+            m.get(f"x{k}", now_us=10)
+    assert len(calls) == 1
+    m.release("c1")
+    m.note_context(m.get("y", now_us=10), 1000)               # the freed slot, now live
+    with pytest.raises(E.PiiError):
+        m.get("z", now_us=10)
+    assert len(calls) == 2                                      # growth retried after a release
 
 
 def test_more_live_conversations_than_slots_match_the_oracle(oracle_cfg):
