@@ -43,6 +43,11 @@ __device__ __forceinline__ uint4 gload16(uintptr_t a) {      // 16-byte aligned 
     const u32x4_t v = *(g_u32x4_t*)a;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// the same at a uniform base + a 32-bit byte offset (the SGPR-base addressing form)
+__device__ __forceinline__ uint4 gload16_at(const uint8_t* base, uint32_t off) {
+    const u32x4_t v = *(g_u32x4_t*)(base + off);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint4 load16(const uint8_t* src, int need_lo, int need_hi) {
     const uintptr_t a = (uintptr_t)src & ~(uintptr_t)15;
     uint4 x = make_uint4(0, 0, 0, 0), y = x;

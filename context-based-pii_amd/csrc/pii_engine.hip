@@ -44,7 +44,13 @@ constexpr int NE_MAX = 2;          // excluder patterns
 #define SCAN_INLINE_HALO 1          // k_scan steps a cut lane's halo itself (no k_halo launch per SCAN group)
 #endif
 constexpr size_t SCAN_LDS_TWO_WG = 80 * 1024;   // k_scan tables up to this: two workgroups per CU
-constexpr int SCAN_BLOCK = 768;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
+#ifndef SCAN1_BLOCK
+#define SCAN1_BLOCK 768
+#endif
+#ifndef SCAN1_WAVES
+#define SCAN1_WAVES 6
+#endif
+constexpr int SCAN_BLOCK = SCAN1_BLOCK;          // 12 waves: two workgroups (<= 80 KiB of tables each) fill the 6 waves/SIMD the VGPRs allow
 constexpr int CTX_BLOCK = 1024;            // (context aggregates are allocated per CTX_BLOCK rows)
 constexpr int SCAN_ITEMS = 8;      // items per thread in the offset scans (blocked, 16-byte accesses)
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
@@ -364,9 +370,60 @@ __device__ __forceinline__ uint32_t lane_bucket(const Geo& g, uint32_t c) {
 
 constexpr uint32_t LANE_SORT_CHUNK = 1024;         // lanes per workgroup (4 per thread; ~1k workgroups at config 2)
 
-// also records every lane's geometry (g.lanes is null here; later kernels read the records)
+// k_scan2's lane split (see k_scan2 below for the design)
+static_assert(BYTES_PER_LANE == 1024, "k_scan2's word rows are sized for 1 KiB lanes");
+constexpr int HB_A = (3 * BYTES_PER_LANE) / 32 + 2;   // word rows of chain A: its half-blocks from its top
+constexpr int HB_B = 32;      // word rows of chain B (from its top, byte s - 1), stored after A's
+
+// The split of a lane for k_scan2: a non-empty utterance start s in (lo, top), not 32-byte aligned (so
+// A's last half-block holds byte s - 1), that makes the longer chain shortest; only lanes no cut
+// touches (their events and arena are the plain ones).  Returns (s - lo) | capA << 16 (capA: the arena
+// entries A may fill -- positions [s, hi - 1], one accept each, + the end-of-text events of its
+// starts), 0 = no split; kmax = half-blocks of the longer chain (the lane's k_scan2 iterations).
+template <class Off>
+__device__ __forceinline__ uint32_t choose_split(const Lane& L, uint32_t top, uint32_t r0, Off uoff, uint32_t& kmax) {
+    const int64_t hb_hi = ((int64_t)top - 1 + r0) >> 5, hb_lo = ((int64_t)L.lo + r0) >> 5;
+    int64_t best = hb_hi - hb_lo + 1, vs = -1, s = 0;
+    if (!L.clo && !L.chi && L.u0 + 1 < L.u1) {
+        int64_t sv = uoff(L.u0 + 1);
+        for (int64_t v = (int64_t)L.u0 + 1; v < (int64_t)L.u1; ++v) {
+            if (sv >= (int64_t)top) break;
+            const int64_t sn = uoff(v + 1);
+            if (sv > (int64_t)L.lo && ((sv + r0) & 31) != 0 && sn != sv) {
+                const int64_t hs = (sv + r0) >> 5;
+                const int64_t na = hb_hi - hs + 1, nb = hs - hb_lo + 1, mx = max(na, nb);
+                if (na <= HB_A && nb <= HB_B && mx < best) {
+                    best = mx;
+                    vs = v;
+                    s = sv;
+                }
+            }
+            sv = sn;
+        }
+    }
+    kmax = (uint32_t)best;
+    if (vs < 0) return 0;
+    const int64_t cap = ((int64_t)top - s) + ((int64_t)L.u1 - vs);
+    if (s - (int64_t)L.lo >= 65536 || cap >= 65536) {
+        kmax = (uint32_t)(hb_hi - hb_lo + 1);
+        return 0;
+    }
+    return (uint32_t)(s - L.lo) | (uint32_t)cap << 16;
+}
+
+// the longer chain's half-blocks of lane L with split sp (the k_scan2 lane order's key)
+__device__ __forceinline__ uint32_t split_kmax(const Lane& L, uint32_t top, uint32_t r0, uint32_t sp) {
+    const uint32_t hb_hi = (top - 1 + r0) >> 5, hb_lo = (L.lo + r0) >> 5;
+    if (!sp) return hb_hi - hb_lo + 1;
+    const uint32_t hs = (L.lo + (sp & 0xffffu) + r0) >> 5;
+    return max(hb_hi - hs + 1, hs - hb_lo + 1);
+}
+
+// also records every lane's geometry (g.lanes is null here; later kernels read the records); SPLIT
+// (k_scan2): also each lane's split (spl), and the lanes are ordered by the longer chain's length
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __restrict__ bucket_cnt,
-                                                    uint4* __restrict__ lanes) {
+                                                    uint4* __restrict__ lanes, uint32_t* __restrict__ spl) {
     __shared__ uint32_t h[LANE_NB];
     for (int i = threadIdx.x; i < LANE_NB; i += blockDim.x) h[i] = 0;
     __syncthreads();
@@ -375,7 +432,13 @@ __global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __res
         const Lane L = g_lane_slow(g, c);
         lanes[c] = lane_pack(L);
         const uint32_t len = L.hi - min(L.lo, L.hi);
-        const uint32_t bk = (uint32_t)(LANE_NB - 1) - min(len >> 5, (uint32_t)(LANE_NB - 1));
+        uint32_t key = len >> 5;
+        if constexpr (SPLIT) {
+            uint32_t km = 0;
+            spl[c] = len ? choose_split(L, L.hi, g.r0, [&](int64_t u) { return g_off(g, (uint32_t)u); }, km) : 0u;
+            key = len ? km : 0u;
+        }
+        const uint32_t bk = (uint32_t)(LANE_NB - 1) - min(key, (uint32_t)(LANE_NB - 1));
         atomicAdd(&h[bk], 1u);
     }
     __syncthreads();
@@ -384,8 +447,10 @@ __global__ __launch_bounds__(256) void k_lane_count(const Geo g, uint32_t* __res
 }
 
 // bucket_cnt[0..NB) = counts (k_lane_count), bucket_cnt[NB..2NB) = reservation cursors (zeroed)
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __restrict__ bucket_cnt,
-                                                    uint32_t* __restrict__ lane_perm, uint32_t* __restrict__ lane_pos) {
+                                                    uint32_t* __restrict__ lane_perm, uint32_t* __restrict__ lane_pos,
+                                                    const uint32_t* __restrict__ spl) {
     constexpr int PER = LANE_SORT_CHUNK / 256;
     __shared__ uint32_t base[LANE_NB], h[LANE_NB];
     if (threadIdx.x < 64) {                        // exclusive prefix of the counts, one wavefront
@@ -408,7 +473,16 @@ __global__ __launch_bounds__(256) void k_lane_place(const Geo g, uint32_t* __res
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t c = c0 + j * 256 + threadIdx.x;
-        bk[j] = c < g.n_chunks ? lane_bucket(g, c) : 0u;
+        bk[j] = 0;
+        if (c < g.n_chunks) {
+            if constexpr (SPLIT) {
+                const Lane L = g_lane(g, c);
+                const uint32_t key = L.hi > L.lo ? split_kmax(L, L.hi, g.r0, spl[c]) : 0u;
+                bk[j] = (uint32_t)(LANE_NB - 1) - min(key, (uint32_t)(LANE_NB - 1));
+            } else {
+                bk[j] = lane_bucket(g, c);
+            }
+        }
         rk[j] = c < g.n_chunks ? atomicAdd(&h[bk[j]], 1u) : 0u;
     }
     __syncthreads();
@@ -584,7 +658,11 @@ __device__ __forceinline__ void scan_emit(Event* __restrict__ ev, uint32_t ab, u
         e.pos = (uint32_t)pos;
         e.sd = (uint16_t)((ad - SCAN_TD_BASE) >> 1);     // transition index (row * CD + class)
         e.sk = (uint16_t)((ak - tk_base) >> 1);
-        ev[(uint64_t)ab + cnt++] = e;
+        // (the index is formed here, opaque to the optimiser: a hoisted 64-bit ev + ab per lane would
+        // hold two VGPRs across the scan loop -- and spill there)
+        uint32_t idx = ab + cnt++;
+        asm volatile("" : "+v"(idx));
+        ev[idx] = e;
     }
 }
 
@@ -716,7 +794,7 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 // window re-scan's small steps, to reach every CU instead of 123: 67 -> 73 us, not kept)
 constexpr int SCAN_BLOCK_WIDE = 1024;
 template <bool HK, int NT = SCAN_BLOCK>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? 6 : 4, NT == SCAN_BLOCK ? 6 : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? SCAN1_WAVES : 4, NT == SCAN_BLOCK ? SCAN1_WAVES : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
@@ -809,6 +887,300 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
     lane_cnt[c] = cnt;
 }
 
+// ------------------------------------------------------------------ k_scan2: two chains per lane
+// k_scan is bound by one dependent LDS read per byte per lane (the D row of byte j is the entry read
+// at byte j + 1): at the 6 waves/SIMD its VGPRs allow, 4.7 achieved, the CU's LDS idles between a
+// wave's dependent reads (issue-active 24%, parked 39%).  k_scan2 gives each lane TWO independent
+// chains.  k_lane_bits2 SPLITS a lane at one of its own utterance starts s near its middle: chain A
+// steps [s, top) exactly as k_scan steps a lane [s, top), chain B steps [lo, s) from the start state --
+// which is the single chain's state after it steps byte s (an utterance start resets both automata),
+// so the split needs no halo and no verification, and the events are exactly the single chain's.
+// The chains step interleaved, byte for byte, over 32-byte half-blocks (a block of text per chain
+// in flight, as k_scan).  A keeps the events at positions >= s, B those < s (a position is reported
+// by the step over the byte before it: A's last half-block holds byte s - 1, as s is not 32-byte
+// aligned).  A writes into the lane's arena, B behind A's capacity; B's events are moved down behind
+// A's at the end, so the arena holds the single chain's events in its order and no consumer changes.
+// A lane without a usable utterance start (a cut lane, one long utterance) runs chain A alone.
+// Register budget (80 VGPRs: 6 waves/SIMD in 768-thread workgroups, two per CU): per byte and chain
+// one history word (both automata's rows, masked, packed; the emission re-derives the byte's class
+// from the text) instead of k_scan's ad / ak, and per chain two 16-byte chunks of text, ping-pong: the
+// next chunk is loaded as soon as the one in its registers has been stepped (no register copies, which
+// would wait for the loads they copy), 16 bytes per chain = 32 interleaved steps ahead of its use.
+// Word rows: k_scan2 runs for 1 KiB lanes with rows longer than 2 KiB cut (long_min), so a lane is
+// shorter than 3 KiB and A's half-blocks always fit HB_A rows -- the loop needs no slow path, and its
+// prefetch is branch-free (a finished chain re-reads its last half-block), so the compiler's counted
+// vmcnt waits stay a whole half-block behind the loads.
+// split[slot] = the lane's split (spl, by lane: k_lane_count); words32 rows [0, HB_A) = A's
+// half-blocks from the lane's top, rows [HB_A, HB_A + HB_B) = B's from byte s - 1
+__global__ __launch_bounds__(256) void k_lane_bits2(const Geo g, const uint32_t* __restrict__ lane_pos,
+                                                    const uint32_t* __restrict__ spl, uint32_t* __restrict__ words,
+                                                    uint32_t* __restrict__ split) {
+    __shared__ uint16_t s_off[4][WROWS_CAP];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t cw0 = c - lane;
+    const uint32_t cw1 = min(cw0 + 64, g.n_chunks);
+    WaveRows W;
+    if (cw0 < g.n_chunks) W.stage(g, cw0, cw1, lane, s_off[wv]);
+    __syncthreads();
+    if (c >= g.n_chunks) return;
+    auto uoff = [&](int64_t u) { return W.off(g, (uint32_t)u); };
+    const Lane L = g_lane(g, c);
+    const uint32_t top = scan_top(g, L);
+    if (top <= L.lo) return;                 // (k_scan2 reads nothing of an empty lane)
+    const uint32_t slot = lane_pos[c];
+    const uint64_t n = g.n_chunks;
+    const int64_t r0 = g.r0;
+    const int64_t vmin = (int64_t)L.u0 + (L.clo ? 1 : 0);
+    const int64_t hb_hi = ((int64_t)top - 1 + r0) >> 5, hb_lo = ((int64_t)L.lo + r0) >> 5;
+    const uint32_t sp = spl[c];
+    split[slot] = sp;
+    auto rows = [&](int64_t h0, int64_t nw, int64_t v, uint64_t row0, bool with_top) {
+        int64_t sv = v >= vmin ? uoff(v) : 0;
+        for (int64_t i = 0; i < nw; ++i) {
+            const int64_t plo = (h0 - i) * 32 - r0;
+            uint32_t bits = 0;
+            if (with_top && i == 0 && (int64_t)top >= plo && (int64_t)top < plo + 32) bits |= 1u << (top - plo);
+            while (v >= vmin && sv >= plo) {
+                if (sv < plo + 32 && uoff(v + 1) > sv) bits |= 1u << (sv - plo);
+                --v;
+                if (v >= vmin) sv = uoff(v);
+            }
+            words[(row0 + (uint64_t)i) * n + slot] = bits;
+        }
+    };
+    if (!sp) {
+        rows(hb_hi, min<int64_t>(hb_hi - hb_lo + 1, HB_A), (int64_t)L.u1 - 1, 0, !L.chi);
+        return;
+    }
+    // the utterance starting at s: the last one starting at or before it (a binary search of its rows)
+    const int64_t s = (int64_t)L.lo + (sp & 0xffffu);
+    int64_t a = vmin, b = (int64_t)L.u1 - 1;
+    while (a < b) {
+        const int64_t m = (a + b + 1) >> 1;
+        if (uoff(m) <= s) a = m;
+        else b = m - 1;
+    }
+    const int64_t hs = (s + r0) >> 5;
+    rows(hb_hi, hb_hi - hs + 1, (int64_t)L.u1 - 1, 0, !L.chi);
+    rows(hs, hs - hb_lo + 1, a, HB_A, false);
+}
+
+// the events of one chain's 8-byte group (scan_emit8's order); h[j] = the masked rows byte j was
+// stepped from (HK: D | K << 16, the class re-derived from the group's text dwords; else the D address)
+template <bool HK>
+__device__ __forceinline__ void scan2_emit8(Event* __restrict__ ev, uint32_t ab, uint32_t& cnt, uint32_t m,
+                                            const uint32_t (&h)[8], uint32_t w_lo, uint32_t w_hi, uint32_t p0,
+                                            uint32_t lo_r, uint32_t len_r, uint32_t tk_base, uint32_t eot_d,
+                                            uint32_t eot_k, uint32_t dsh) {
+    do {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        const uint32_t j = 7u - (b >> 1);
+        const uint32_t hj = sel8(h, j);
+        uint32_t a, k;
+        if (HK) {
+            const uint32_t by = (((j & 4u) ? w_hi : w_lo) >> (8u * (j & 3u))) & 0xffu;
+            const uint32_t cw = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)(4u * by));
+            a = (hj & 0xffffu) + (cw & 0xffffu);
+            k = (hj >> 16) + (cw >> 16);
+        } else {
+            a = hj;
+            k = tk_base;
+        }
+        uint32_t pos = p0 + j + 1u;
+        if (b & 1u) {
+            a = ((lds_u16(a) & 0xfffcu) << dsh) + eot_d;
+            k = (lds_u16(k) & 0xfffcu) + eot_k;
+            pos -= 1u;
+        }
+        scan_emit(ev, ab, cnt, pos, lo_r, len_r, a, k, tk_base);
+    } while (m);
+}
+
+// one byte of chain X (J: byte of the group, BIT: its bit in the half-block word)
+#define S2_STEP1(X, J, BIT)                                                                       \
+    {                                                                                             \
+        if (HK) {                                                                                 \
+            h##X[J] = ((nk##X << 16) | nd##X) & ~pm##X & 0xfffcfffcu;                             \
+            uint32_t ad_, ak_;                                                                    \
+            asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0" \
+                : "=v"(ad_) : "v"(h##X[J]), "v"(c##X[J]));                                       \
+            asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1" \
+                : "=v"(ak_) : "v"(h##X[J]), "v"(c##X[J]));                                       \
+            nd##X = lds_u16(ad_);                                                                 \
+            nk##X = lds_u16(ak_);                                                                 \
+            m##X = __builtin_amdgcn_alignbit(nd##X | nk##X, m##X, 2);                             \
+        } else {                                                                                  \
+            h##X[J] = ((nd##X & ~pm##X & 0xfffcu) << dsh) + c##X[J];                              \
+            nd##X = lds_u16(h##X[J]);                                                             \
+            m##X = __builtin_amdgcn_alignbit(nd##X, m##X, 2);                                     \
+        }                                                                                         \
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(pm##X) : "v"(b##X), "n"(BIT));                      \
+    }
+
+#define S2_CLASSES8(C, W, H)                                                                      \
+    C[0] = class_of<(H) + 0>(W);                                                                  \
+    C[1] = class_of<(H) + 1>(W);                                                                  \
+    C[2] = class_of<(H) + 2>(W);                                                                  \
+    C[3] = class_of<(H) + 3>(W);                                                                  \
+    C[4] = class_of<(H) + 4>(W);                                                                  \
+    C[5] = class_of<(H) + 5>(W);                                                                  \
+    C[6] = class_of<(H) + 6>(W);                                                                  \
+    C[7] = class_of<(H) + 7>(W);
+
+#define S2_STEP2(J, BIT) S2_STEP1(A, J, BIT) S2_STEP1(B, J, BIT)
+
+// one 8-byte group of both chains: bytes H..H+7 of chunk WA / WB, at bit OFF + H of the words
+#define S2_GROUP(WA, WB, H, OFF)                                                                  \
+    {                                                                                             \
+        uint32_t cA[8], cB[8], hA[8], hB[8], mA = 0, mB = 0;                                      \
+        S2_CLASSES8(cA, WA, H)                                                                    \
+        S2_CLASSES8(cB, WB, H)                                                                    \
+        const uint32_t mkA = aliveA ? lds_u16(spread + 2u * ((bA >> ((OFF) + (H))) & 0xffu)) : 0u; \
+        const uint32_t mkB = aliveB ? lds_u16(spread + 2u * ((bB >> ((OFF) + (H))) & 0xffu)) : 0u; \
+        S2_STEP2(7, (OFF) + (H) + 7) S2_STEP2(6, (OFF) + (H) + 6)                                 \
+        S2_STEP2(5, (OFF) + (H) + 5) S2_STEP2(4, (OFF) + (H) + 4)                                 \
+        S2_STEP2(3, (OFF) + (H) + 3) S2_STEP2(2, (OFF) + (H) + 2)                                 \
+        S2_STEP2(1, (OFF) + (H) + 1) S2_STEP2(0, (OFF) + (H) + 0)                                 \
+        mA = (mA >> 16) & mkA;                                                                    \
+        mB = (mB >> 16) & mkB;                                                                    \
+        if (__builtin_expect((mA | mB) != 0, 0)) {                                                \
+            if (mA)                                                                               \
+                scan2_emit8<HK>(ev, abA, cntA, mA, hA, (H) ? WA.z : WA.x, (H) ? WA.w : WA.y,       \
+                                bposA + (OFF) + (H), sA, ehi - sA, tk_base, eot_d, eot_k, dsh);   \
+            if (mB)                                                                               \
+                scan2_emit8<HK>(ev, abB, cntB, mB, hB, (H) ? WB.z : WB.x, (H) ? WB.w : WB.y,       \
+                                bposB + (OFF) + (H), lo_r, sA - 1u - lo_r, tk_base, eot_d, eot_k, dsh); \
+        }                                                                                         \
+    }
+
+#ifndef SCAN2_BLOCK
+#define SCAN2_BLOCK 768
+#endif
+#ifndef SCAN2_WAVES
+#define SCAN2_WAVES 6
+#endif
+template <bool HK, int NT = SCAN2_BLOCK>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN2_BLOCK ? SCAN2_WAVES : 4, NT == SCAN2_BLOCK ? SCAN2_WAVES : 4))) void k_scan2(
+    const RulesDev R, const Geo g, const uint8_t* __restrict__ text, const uint32_t* __restrict__ words,
+    const uint32_t* __restrict__ split, const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
+    uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st, const uint32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+    if (*err & ERR_ARGS) return;
+    const int nd_words = R.SD * R.CDs / 2;
+    const int nk_words = R.SK * R.CKs / 2;
+    const uint32_t tk_base = SCAN_TD_BASE + (uint32_t)nd_words * 4;
+    {
+        const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
+        const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
+        uint32_t* d_td = smem32 + SCAN_TD_BASE / 4;
+        uint32_t* d_tk = d_td + nd_words;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
+        for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
+        for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
+        uint32_t* d_sp = d_tk + nk_words;
+        for (int i = threadIdx.x; i < 128; i += blockDim.x) d_sp[i] = scan_spread(2 * i) | scan_spread(2 * i + 1) << 16;
+    }
+    __syncthreads();
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
+    if (t >= g.n_chunks) return;
+    const uint32_t c = lane_perm[t];
+    const Lane L = g_lane(g, c);
+    const uint32_t top = scan_top(g, L);
+    const uint32_t end_r = (uint32_t)g_off(g, g.n_utt);
+    uint32_t cnt = 0;
+    if (top > L.lo) {
+        uint32_t lo_r, len_r;
+        emit_range(L, lo_r, len_r);
+        const uint32_t ab = (uint32_t)ev_base(L, c);
+        const uint32_t eot_d = SCAN_TD_BASE + 2u * (uint32_t)(R.CD - 1), eot_k = tk_base + 2u * (uint32_t)(R.CK - 1);
+        const uint32_t spread = tk_base + (uint32_t)nk_words * 4;
+        const uint32_t dsh = HK ? 0u : (uint32_t)R.dsh;
+        const uint32_t sp = split[t];
+        const uint32_t s = L.lo + (sp & 0xffffu);        // (lo when not split)
+        const uint32_t abA = ab, abB = ab + (sp >> 16);
+        // emission ranges: A [sA, ehi] ([s, e_hi] when split, the lane's own otherwise), B [lo_r, s - 1]
+        const uint32_t sA = sp ? s : lo_r, ehi = lo_r + len_r;
+        uint32_t ndA = 0, nkA = 0, pmA = 0xffffffffu, ndB = 0, nkB = 0, pmB = 0xffffffffu;
+        if (L.chi) {             // (never split)
+#if SCAN_INLINE_HALO
+            const uint32_t hs = halo_state(R, g, text, L);
+            lane_st[2 * c] = hs;
+#else
+            const uint32_t hs = lane_st[2 * c];
+#endif
+            ndA = hs & 0xffffu;
+            nkA = hs >> 16;
+            pmA = 0;
+        }
+        const uint32_t r0 = g.r0;
+        const uintptr_t tpb = (uintptr_t)(text + g.base) - r0;
+        const uint32_t hbA = (top - 1 + r0) >> 5, hb_lo = (L.lo + r0) >> 5;
+        const uint32_t hs = sp ? (s + r0) >> 5 : hb_lo;
+        const uint32_t nA = hbA - hs + 1, nB = sp ? hs - hb_lo + 1 : 0, hbB = hs;
+        const uint32_t q_end = (end_r - 1 + r0) >> 4;             // last chunk with a batch byte
+        const uint32_t n = g.n_chunks;           // (word rows * lanes < 2^32: rows < 2^8, lanes < 2^23)
+        // the top half-block: its upper chunk only when it holds a batch byte (then every load is
+        // unconditional: a finished chain re-reads its last half-block, its start bits forced to ones;
+        // a chunk past the batch end is never read -- a top half-block's upper chunk is replaced by its
+        // lower one, whose bytes then step only as garbage of a finished chain)
+        // (uniform base + 32-bit offsets: the loads take the SGPR-base form, no 64-bit address VGPRs)
+        const uint8_t* const tbase = reinterpret_cast<const uint8_t*>(tpb);
+        auto ld = [&](uint32_t off) { return gload16_at(tbase, off); };
+        auto hi16 = [&](uint32_t hb) { return hb * 32u + (2 * hb + 1 <= q_end ? 16u : 0u); };
+        auto lo16 = [&](uint32_t hb) { return hb * 32u; };
+        uint4 PA = make_uint4(0, 0, 0, 0);
+        if (2 * hbA + 1 <= q_end) PA = ld(lo16(hbA) + 16);
+        uint4 QA = ld(lo16(hbA)), PB = ld(hi16(hbB)), QB = ld(lo16(hbB));
+        // (the lane's counts are re-derived per use: registers decide this kernel's occupancy)
+#define LAST_A (nA - 1)
+#define LAST_B (nB ? nB - 1 : 0u)
+        uint32_t wA = words[t], wB = words[(uint32_t)HB_A * n + t];
+        uint32_t nwA = words[min(1u, LAST_A) * n + t], nwB = words[(HB_A + min(1u, LAST_B)) * n + t];
+        uint32_t cntA = 0, cntB = 0;
+        for (uint32_t k = 0;; ++k) {
+            const bool aliveA = k < nA, aliveB = k < nB;      // (lane masks: no VGPRs)
+            const uint32_t bA = aliveA ? wA : 0xffffffffu, bB = aliveB ? wB : 0xffffffffu;
+            const uint32_t ka = min(k + 1, LAST_A), kb = min(k + 1, LAST_B);
+            const uint32_t bposA = 32u * (hbA - k) - r0, bposB = 32u * (hbB - k) - r0;
+            S2_GROUP(PA, PB, 8, 16)
+            S2_GROUP(PA, PB, 0, 16)
+            PA = ld(hi16(hbA - ka));
+            PB = ld(hi16(hbB - kb));
+            S2_GROUP(QA, QB, 8, 0)
+            S2_GROUP(QA, QB, 0, 0)
+            QA = ld(lo16(hbA - ka));
+            QB = ld(lo16(hbB - kb));
+            wA = nwA;
+            wB = nwB;
+            nwA = words[min(k + 2, LAST_A) * n + t];
+            nwB = words[(HB_A + min(k + 2, LAST_B)) * n + t];
+            if (k + 1 >= max(nA, nB)) break;
+        }
+#undef LAST_A
+#undef LAST_B
+        // (the lane's id and cut flag re-read: nothing but the chains' state stays live across the loop)
+        if (g.lanes[lane_perm[t]].z >> 31)                              // cut at lo: never split,
+            lane_st[2 * lane_perm[t] + 1] = scan_state(ndA, nkA);       // A ended at byte lo
+        if (cntB && abA + cntA < abB) {         // B's events behind A's (ascending: the target is lower)
+            const uint2* src = reinterpret_cast<const uint2*>(ev + abB);
+            uint2* dst = reinterpret_cast<uint2*>(ev + abA + cntA);
+            for (uint32_t i = 0; i < cntB; i += 4) {
+                uint2 x[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (i + r < cntB) x[r] = src[i + r];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (i + r < cntB) dst[i + r] = x[r];
+            }
+        }
+        cnt = cntA + cntB;
+    }
+    lane_cnt[lane_perm[t]] = cnt;
+}
+
 // ---- k_scan_fix: stitching of cut rows.  A lane cut at hi scanned SCAN_HALO bytes past the cut from
 // the start state; when that did not reproduce the state its right neighbour really ends with (a
 // context longer than the halo: a long unbroken token), the lane is re-scanned from the true state.
@@ -862,6 +1234,11 @@ constexpr int FIX_Q = 512;
 // LDS past the scan tables (the tables' entries are absolute LDS addresses, so the kernel declares no
 // static LDS): queue, entry states, previous round's lanes, counters
 constexpr size_t FIX_LDS = (3 * FIX_Q + 4) * 4;
+#if !SCAN_INLINE_HALO && defined(SCAN_STREAMS) && SCAN_STREAMS > 1
+// k_halo of group q runs on the engine stream after the fork; k_scan of that group on an aux stream
+// that waits only on the fork: the scan would read halo states before k_halo writes them
+#error "SCAN_STREAMS > 1 needs SCAN_INLINE_HALO (k_scan steps its own halo)"
+#endif
 #ifndef SCAN_STREAMS
 #define SCAN_STREAMS 3                // streams for several SCAN groups' passes (config 5, wall per step, one box:
                                       // 1 / 2 / 3 -> 6.65 / 6.31 / 6.28 ms)
@@ -3004,9 +3381,18 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
 // LDS.  A tile with more spans than the piece table holds is assembled in several passes.  Rows of
 // any length (a whole transcript) take the same path.
 constexpr int REDACT_BLOCK = 256;
+#ifndef REDACT_ABLATE
+#define REDACT_ABLATE 0             // measurement builds only: 1 = k_redact without its assembly loop
+#endif
+#ifndef REDACT_PIPE
+#define REDACT_PIPE 1               // tile_assemble's pipelined interior-block loop (0: one block at a time)
+#endif
 constexpr int PIECE_MAX = 1024;
-constexpr int BLK_MAX = 4096;       // output blocks (64 KiB) covered by the block -> piece table
-constexpr uint32_t RTILE_SHIFT = 16;  // output tile: 64 KiB = BLK_MAX blocks
+#ifndef RTILE_SHIFT_N
+#define RTILE_SHIFT_N 16
+#endif
+constexpr uint32_t RTILE_SHIFT = RTILE_SHIFT_N;  // output tile: 64 KiB = BLK_MAX blocks
+constexpr int BLK_MAX = 1 << (RTILE_SHIFT - 4);  // output blocks covered by the block -> piece table
 constexpr int SPAN_PASS = REDACT_BLOCK - 1;   // spans per assembly pass: one per thread (2 pieces each + 2 <= PIECE_MAX)
 
 struct RSpan {          // one kept span in batch order (16 B)
@@ -3129,6 +3515,78 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
                 if (j >= k.b_lo && j < k.b_hi) ob[j] = (uint8_t)(vw[j >> 2] >> (8 * (j & 3)));
         }
     };
+#if REDACT_PIPE
+    if (table) {
+        // Interior blocks (all 16 bytes in [out_lo, out_hi)) in a software pipeline: block q + 256's
+        // piece lookup and its two source loads are issued before block q is merged and stored.  Every
+        // load and store is unconditional (a chunk holding no byte of the piece is replaced by the
+        // chunk that does, so no address leaves the source buffer), so the compiler's vmcnt waits are
+        // counted and the next block's loads stay in flight -- a conditional load makes every wait a
+        // vmcnt(0) (why two-blocks-per-iteration forms measured slower in rounds 3-4).  A block whose
+        // bytes come from several pieces (~3% of them: the blocks around a token) is stored from its
+        // first piece here and rebuilt by the general path after the loop (same thread, later store).
+        const int64_t qa = q_lo + (((out_lo + omis) & 15) ? 1 : 0);
+        const int64_t qb = q_hi - (((out_hi + omis) & 15) ? 1 : 0);
+        struct Fast {
+            uint4 x, y;
+            uint32_t sh;
+            bool one;
+        };
+        static_assert(BLK_MAX / REDACT_BLOCK <= 32, "fix mask: one bit per interior block of a thread");
+        auto fetch = [&](Fast& f, int64_t q) {
+            const uint32_t pi = s_bp[q - q_lo];
+            const int64_t r0 = q * 16 - omis - out_lo;
+            const uint32_t qs = s_pout[pi], qe = s_pout[pi + 1];
+            const uintptr_t a = (uintptr_t)s_psrc[pi] + (uintptr_t)(r0 - (int64_t)qs);
+            const uintptr_t a0 = a & ~(uintptr_t)15;
+            f.sh = (uint32_t)(a & 15);
+            f.one = (int64_t)qe >= r0 + 16;
+            const bool two = f.sh + (f.one ? 16u : (uint32_t)((int64_t)qe - r0)) > 16u;
+            f.x = gload16(a0);
+            f.y = gload16(two ? a0 + 16 : a0);
+        };
+        uint32_t fix = 0;                 // bit i: this thread's i-th interior block needs the general path
+        const int64_t q0 = qa + tid;
+        if (q0 <= qb) {
+            // ping-pong buffers (no register copy: a copy would wait for the loads it copies); past
+            // the thread's last block a buffer re-reads and re-stores that block (the same bytes)
+            const int64_t ql = q0 + ((qb - q0) / REDACT_BLOCK) * REDACT_BLOCK;
+            auto put = [&](const Fast& f, int64_t q) {
+                const uint4 v = window16(f.x, f.y, f.sh);
+                u32x4_t nv = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(nv, reinterpret_cast<u32x4_t*>(op + q));
+                if (!f.one) fix |= 1u << (uint32_t)((q - q0) / REDACT_BLOCK);
+            };
+            Fast f0, f1;
+            fetch(f0, q0);
+            for (int64_t q = q0; q <= ql; q += 2 * REDACT_BLOCK) {
+                const int64_t q1 = min<int64_t>(q + REDACT_BLOCK, ql), q2 = min<int64_t>(q + 2 * REDACT_BLOCK, ql);
+                fetch(f1, q1);
+                put(f0, q);
+                fetch(f0, q2);
+                put(f1, q1);
+            }
+        }
+        // the edge blocks and the multi-piece ones
+        if (tid == 0 && qa > q_lo) {
+            Blk k;
+            begin(k, q_lo);
+            finish(k, q_lo);
+        }
+        if (tid == REDACT_BLOCK - 1 && qb < q_hi && q_hi >= qa) {
+            Blk k;
+            begin(k, q_hi);
+            finish(k, q_hi);
+        }
+        for (; fix; fix &= fix - 1) {
+            const int64_t qf = qa + tid + (int64_t)__builtin_ctz(fix) * REDACT_BLOCK;
+            Blk k;
+            begin(k, qf);
+            finish(k, qf);
+        }
+        return;
+    }
+#endif
     for (int64_t q = q_lo + tid; q <= q_hi; q += REDACT_BLOCK) {
         Blk k;
         begin(k, q);
@@ -3328,7 +3786,9 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
             s_pout[1] = (uint32_t)(hi - lo);
         }
         __syncthreads();
+#if REDACT_ABLATE != 1
         tile_assemble(s_pout, s_psrc, n == 0 ? 1u : 2 * n + 1, s_bp, s_wsum, out, lo, hi);
+#endif
         __syncthreads();
         i += n;
         lo = hi;
@@ -4373,6 +4833,9 @@ struct pii_engine {
     uint32_t* lane_bkt = nullptr;      // [2 * LANE_NB] bucket counts + reservation cursors
     uint32_t* lane_cnt = nullptr;
     uint64_t* bnd = nullptr;
+    uint32_t* lane_split = nullptr;    // k_scan2: per slot split point | A's arena capacity (k_lane_bits2)
+    uint32_t* lane_spl = nullptr;      // the same per lane (k_lane_count)
+    bool scan2 = false;                // two chains per lane in the SCAN (PII_SCAN2=1: k_scan2; slower)
     EvLoc* evloc = nullptr;
     uint64_t ev_cap = 0;
     uint64_t* lane_ev = nullptr;      // exclusive scan of lane_cnt: first dense event index per lane
@@ -4572,7 +5035,11 @@ int ensure_scratch(pii_engine* e, uint32_t n_utt, uint64_t bytes, uint32_t n_lan
         if ((rc = grow(e, e->lane_cnt, nl * e->n_sg))) return rc;
         if (e->n_sg > 1 && (rc = grow(e, e->lane_evn, nl))) return rc;
         if ((rc = grow(e, e->lane_ev, nl))) return rc;
-        if ((rc = grow(e, e->bnd, nl * LANE_WORDS))) return rc;
+        // utterance-start words: k_scan's u64 per block (LANE_WORDS rows) or k_scan2's u32 per
+        // half-block (HB_A + HB_B rows), one buffer for either
+        if ((rc = grow(e, e->bnd, nl * std::max<uint64_t>(LANE_WORDS, (HB_A + HB_B) / 2)))) return rc;
+        if ((rc = grow(e, e->lane_split, nl))) return rc;
+        if ((rc = grow(e, e->lane_spl, nl))) return rc;
         if ((rc = grow(e, e->lane_pair, nl))) return rc;
         if ((rc = grow(e, e->lane_np, nl))) return rc;
         if ((rc = grow(e, e->lane_st, 2 * nl * e->n_sg))) return rc;
@@ -4750,12 +5217,18 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_fill_long<<<row_grid(e, total_bytes), 256, 0, st>>>(offs, n_utt, n_chunks, e->lane_shift, e->r0, e->long_rows,
                                                                    e->long_count, (uint32_t)e->cap_long, e->first_utt);
         if (n_chunks > 0) {
+            // two chains per lane (k_scan2) for batches of full-size lanes; small batches (a re-scan
+            // step: 128-512-byte lanes of one or two rows) have no utterance start to split at
+            const bool split = e->scan2 && e->lane_shift == (uint32_t)__builtin_ctz(BYTES_PER_LANE) &&
+                               e->long_min != NO_CUTS && e->n_sg == 1;
             HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
             Geo g0 = g;
             g0.lanes = nullptr;
-            k_lane_count<<<nsb, 256, 0, st>>>(g0, e->lane_bkt, e->lane_geo);
-            k_lane_place<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm, e->lane_pos);
+            (split ? k_lane_count<true> : k_lane_count<false>)<<<nsb, 256, 0, st>>>(g0, e->lane_bkt, e->lane_geo,
+                                                                                    e->lane_spl);
+            (split ? k_lane_place<true> : k_lane_place<false>)<<<nsb, 256, 0, st>>>(g, e->lane_bkt, e->lane_perm,
+                                                                                    e->lane_pos, e->lane_spl);
             // one pass per SCAN group (one for the shipped rules): halo states, scan, stitching; the
             // utterance-start words are written once.  Several groups: group q on stream q mod
             // SCAN_STREAMS (forked after the words, joined before the pairs), so one pass's tail -- the
@@ -4767,7 +5240,12 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 Event* evq = e->ev + (uint64_t)q * e->cap_ev;
                 uint32_t* cq = e->lane_cnt + (uint64_t)q * e->cap_lanes;
                 uint32_t* stq = e->lane_st + 2ull * q * e->cap_lanes;
-                if (q == 0) k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
+                if (q == 0 && split)
+                    k_lane_bits2<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->lane_spl,
+                                                                         reinterpret_cast<uint32_t*>(e->bnd),
+                                                                         e->lane_split);
+                else if (q == 0)
+                    k_lane_bits<<<(n_chunks + 255) / 256, 256, 0, st>>>(g, e->lane_pos, e->bnd);
                 if (!SCAN_INLINE_HALO && e->long_min != NO_CUTS)
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
@@ -4785,9 +5263,17 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 // table); only the dictionary groups' ~100 KB tables need one 1024-thread workgroup
                 const bool one_wg = e->sg_lds[q] > SCAN_LDS_TWO_WG;
                 const int nt = one_wg ? SCAN_BLOCK_WIDE : SCAN_BLOCK;
-                (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
-                    (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], sq>>>(
-                    Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
+                if (split) {
+                    const int nt2 = one_wg ? SCAN_BLOCK_WIDE : SCAN2_BLOCK;
+                    (q == 0 ? k_scan2<true> : one_wg ? k_scan2<false, SCAN_BLOCK_WIDE> : k_scan2<false>)<<<
+                        (n_chunks + nt2 - 1) / nt2, nt2, e->sg_lds[q], sq>>>(
+                        Rq, g, text, reinterpret_cast<const uint32_t*>(e->bnd), e->lane_split, e->lane_perm, evq,
+                        cq, stq, e->d_err);
+                } else {
+                    (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
+                        (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], sq>>>(
+                        Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
+                }
             }
             for (uint32_t i = 0; i + 1 < ns_scan; ++i) {
                 HIPCHK(hipEventRecord(e->ev_join[i], e->aux[i]));
@@ -5765,6 +6251,15 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             hipMemcpy(e->d_sg_lds, lds32.data(), lds32.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
             return fail("hipMalloc failed");
     }
+    if (const char* v = std::getenv("PII_SCAN2")) e->scan2 = std::atoi(v) != 0;
+    if (max_lds > 64 * 1024 &&
+        (hipFuncSetAttribute((const void*)k_scan2<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan2<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_scan2<false, SCAN_BLOCK_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)max_lds) != hipSuccess))
+        return fail("cannot raise LDS limit");
     if (max_lds > 64 * 1024 &&
         (hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
@@ -5823,7 +6318,7 @@ int pii_engine_destroy(pii_engine* e) {
     if (!e) return PII_E_ARG;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     void* ptrs[] = {e->d_rules, e->st_group, e->st_ts, e->stamp, e->ev, e->fd, e->n_ev, e->n_find,
-                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->hist_part, e->evloc, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
+                    e->out_len, e->incl, e->agg_f, e->first_utt, e->lane_perm, e->lane_pos, e->lane_bkt, e->lane_cnt, e->bnd, e->lane_split, e->lane_spl, e->hist_part, e->evloc, e->lane_ev, e->pres, e->pend, e->lane_pair, e->lane_np, e->matched, e->mcount, e->cont,
                     e->img_first.d, e->img_first_hot.d, e->img_eval.d, e->img_eval_rg.d, e->img_sel.d, e->img_sel_rg.d, e->kw, e->ctx, e->agg_v, e->commit,
                     e->span_offs, e->bsum, e->out_offs_tmp, e->lb_state, e->lb_ticket, e->d_err, e->d_totals, e->h_text, e->h_role,
                     e->h_out, e->h_offs, e->h_out_offs, e->h_slot, e->h_ts, e->h_spans, e->h_ctx,
