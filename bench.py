@@ -280,7 +280,36 @@ def reduce_over_ranks(dist, dev, elapsed: float, local_hist: np.ndarray, sums=()
     return float(t[0].item()), [float(x) for x in t[1:].tolist()], reduced, verified
 
 
-def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None, bank=None):
+def one_stream_scan_ms(B, make_engine, C, steps: int = 3) -> float:
+    """k_scan device time per step with every SCAN group's pass on ONE stream (PII_SCAN_STREAMS=1,
+    read at engine creation): the passes then run back to back, so the span between the events around
+    the scan stage is the sum of the per-pass kernel times.  (With the passes on three streams the
+    span is a wall-clock interval in which passes overlap: not a per-kernel time -- VERDICT r5.)"""
+    old = os.environ.get("PII_SCAN_STREAMS")
+    os.environ["PII_SCAN_STREAMS"] = "1"
+    try:
+        eng = make_engine(B, None, C)
+    finally:
+        if old is None:
+            del os.environ["PII_SCAN_STREAMS"]
+        else:
+            os.environ["PII_SCAN_STREAMS"] = old
+    tot = 0.0
+    try:
+        for i in range(steps + 1):
+            B.run(eng)
+            _, _, fl = eng.sync()
+            if fl:
+                raise RuntimeError(f"engine error flags {fl}")
+            if i:                                  # (the first call sizes the work buffers)
+                tot += eng.kernel_timings()["k_scan"]
+    finally:
+        eng.close()
+    return tot / steps
+
+
+def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None, bank=None,
+             one_stream_probe: bool = False):
     """One rank of the config-2 benchmark: shard -> W warmup steps -> K timed steps between barriers
     + device syncs -> max-over-ranks time.  A step = one scan+redact pass over the rank's resident
     shard + the all-reduce of the u64[T+1] per-infoType histogram (the only collective; reset every
@@ -338,6 +367,10 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
     eng.close()
     if rank != 0:
         return None
+    scan_wall_ms = None
+    if one_stream_probe:         # (after the timed region: per-pass k_scan time for the roofline)
+        scan_wall_ms = k_ms["k_scan"]
+        k_ms["k_scan"] = one_stream_scan_ms(B, make_engine, C)
     n, n_bytes = B.n, B.n_bytes
     n_lanes = (n_bytes + LANE_BYTES - 1) // LANE_BYTES
     ms_step = elapsed / args.steps * 1e3
@@ -378,6 +411,11 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
         "stages_ms": {k: round(float(v), 4) for k, v in zip(
             ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
         "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
+        **({"scan_stage_wall_ms": round(scan_wall_ms, 4),
+            "scan_stage_note": "kernels_ms.k_scan and roofline.launch_ms: the SCAN passes' kernel time, from "
+                               "an engine with the passes on one stream (PII_SCAN_STREAMS=1, after the timed "
+                               "region); scan_stage_wall_ms: the wall span of the overlapped passes in the "
+                               "timed steps (three streams)"} if scan_wall_ms is not None else {}),
         "pipeline": {"algorithmic_bytes": int(Bw), "GBps": round(Bw / t_pipe / 1e9, 1),
                      "frac": round(Bw / t_pipe / 1e9 / HBM_PEAK_GBPS, 4), "traffic": pipe_traffic},
         "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(scan_GBps, 1), "peak": HBM_PEAK_GBPS,
@@ -870,7 +908,8 @@ def config5_main(args):
 
     def make_engine(batch, bank_, C):
         return eng_mod.Engine(comp.blob, device=local, n_conv_slots=C)
-    line = run_rank(args, rank, world, dev, make_engine, cpu=cpu, dist=dist if world > 1 else None, bank=bank)
+    line = run_rank(args, rank, world, dev, make_engine, cpu=cpu, dist=dist if world > 1 else None, bank=bank,
+                    one_stream_probe=len(comp.scan_groups) > 1)
     if rank == 0:
         line["metric"] = "config 5: transcript MB/s scanned+redacted per node with 500+ custom infoTypes"
         line["l2"] = measured_l2()

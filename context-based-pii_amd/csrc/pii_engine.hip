@@ -3382,7 +3382,7 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
 // any length (a whole transcript) take the same path.
 constexpr int REDACT_BLOCK = 256;
 #ifndef REDACT_ABLATE
-#define REDACT_ABLATE 0             // measurement builds only: 1 = k_redact without its assembly loop
+#define REDACT_ABLATE 0             // measurement builds only: 1 = no assembly, 2 = tables only, 3 = no source loads
 #endif
 #ifndef REDACT_PIPE
 #define REDACT_PIPE 1               // tile_assemble's pipelined interior-block loop (0: one block at a time)
@@ -3448,6 +3448,9 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
         __syncthreads();
     }
     if (total_p == 0) return;
+#if REDACT_ABLATE == 2
+    return;                          // (measurement: tables only)
+#endif
     uint4* __restrict__ op = reinterpret_cast<uint4*>(out - omis);
     const int64_t span = out_hi - out_lo;
     // a block's first piece is loaded before the loop over its further pieces (those are rare); two
@@ -3542,8 +3545,14 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
             f.sh = (uint32_t)(a & 15);
             f.one = (int64_t)qe >= r0 + 16;
             const bool two = f.sh + (f.one ? 16u : (uint32_t)((int64_t)qe - r0)) > 16u;
+#if REDACT_ABLATE == 3
+            f.x = make_uint4((uint32_t)a0, 0, 0, 0);      // (measurement: no source loads)
+            f.y = f.x;
+            (void)two;
+#else
             f.x = gload16(a0);
             f.y = gload16(two ? a0 + 16 : a0);
+#endif
         };
         uint32_t fix = 0;                 // bit i: this thread's i-th interior block needs the general path
         const int64_t q0 = qa + tid;
