@@ -280,6 +280,26 @@ def reduce_over_ranks(dist, dev, elapsed: float, local_hist: np.ndarray, sums=()
     return float(t[0].item()), [float(x) for x in t[1:].tolist()], reduced, verified
 
 
+STAGES_NOTE = ("stages_ms: stage boundaries from HIP events (timing level 2) on 3 steps after the timed region "
+               "(in the timed steps the engine records only the call's start / end and the events around "
+               "k_scan and k_redact: each event between kernels costs the stream ~6 us); pipeline.GBps uses the "
+               "timed steps' start-to-completion time")
+
+
+def stage_probe(eng, step, n: int = 3):
+    """per-stage device times (pii_last_timings [0..5] at timing level 2) averaged over n further
+    calls of `step`; the engine is left at level 1"""
+    eng.set_timing(2)
+    acc = np.zeros(6)
+    try:
+        for i in range(n):
+            step(i)
+            acc += np.array(eng.timings())
+    finally:
+        eng.set_timing(1)
+    return acc / n
+
+
 def one_stream_scan_ms(B, make_engine, C, steps: int = 3) -> float:
     """k_scan device time per step with every SCAN group's pass on ONE stream (PII_SCAN_STREAMS=1,
     read at engine creation): the passes then run back to back, so the span between the events around
@@ -362,6 +382,7 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
         verified = verified and bool((hist.cpu().numpy() == reduced).all())
     per_stage /= args.steps
     k_ms = {k: v / args.steps for k, v in k_ms.items()}
+    stages = stage_probe(eng, lambda i: step())
     n_pairs, n_events = eng.queue_sizes()
     names = list(eng.type_names)
     eng.close()
@@ -409,7 +430,8 @@ def run_rank(args, rank: int, world: int, dev, make_engine, cpu=None, dist=None,
         "spans_per_step_per_gpu": int(ns),
         "queues_per_step_per_gpu": {"scan_events": n_events, "candidate_pairs": n_pairs},
         "stages_ms": {k: round(float(v), 4) for k, v in zip(
-            ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], per_stage)},
+            ["scan+pairs", "context", "resolve", "offsets", "redact", "pipeline"], stages)},
+        "stages_note": STAGES_NOTE,
         "kernels_ms": {k: round(v, 4) for k, v in k_ms.items()},
         **({"scan_stage_wall_ms": round(scan_wall_ms, 4),
             "scan_stage_note": "kernels_ms.k_scan and roofline.launch_ms: the SCAN passes' kernel time, from "
@@ -1195,6 +1217,7 @@ def window_main(args):
     K = args.steps
     per_stage /= K
     k_red /= K
+    stages = stage_probe(eng, lambda i: step(warm + K + i)) if warm + K + 3 <= U else per_stage
     # window bytes read to write the outputs: every window's utterances and separators
     lens = (meta.offsets[1:] - meta.offsets[:-1]).astype(np.int64).reshape(U, C)
     win_in = 0
@@ -1225,7 +1248,8 @@ def window_main(args):
         "naive_equivalent_bytes_rescanned_per_step": int(win_in / K),
         "new_bytes_per_step": int(new_b / K),
         "stages_ms": {k: round(float(v), 4) for k, v in zip(
-            ["scan+pairs", "context", "first+cands", "select+offsets", "redact+commit", "pipeline"], per_stage)},
+            ["scan+pairs", "context", "first+cands", "select+offsets", "redact+commit", "pipeline"], stages)},
+        "stages_note": STAGES_NOTE,
         "pipeline": {"algorithmic_bytes": int(B / K), "GBps": round(B / t_pipe / 1e9, 1),
                      "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4),
                      "traffic": measured_pipeline_traffic(int(meta.offsets[-1]), "window")},

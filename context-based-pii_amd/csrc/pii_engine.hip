@@ -3253,16 +3253,37 @@ __device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t status, uin
     return ((uint64_t)(epoch & 0xffffffu) << 40) | (status << 38) | (v & ((1ull << 38) - 1));
 }
 
-__global__ __launch_bounds__(LB_BLOCK) void k_scan_lb(const uint32_t* __restrict__ in, uint32_t n,
-                                                      uint64_t* __restrict__ out, unsigned long long* state,
-                                                      unsigned long long* ctr, uint32_t epoch) {
+// up to two independent scans in one launch (blockIdx.y: its own input, tiles, tile states and
+// ticket pair); a block whose ticket is past its scan's tiles only counts itself out
+struct LbArgs {
+    const uint32_t* in[2];
+    uint64_t* out[2];
+    uint32_t n[2], nb[2];
+    uint32_t sstride;        // tile-state words per scan
+};
+
+__global__ __launch_bounds__(LB_BLOCK) void k_scan_lb(const LbArgs a, unsigned long long* state0,
+                                                      unsigned long long* ctr0, uint32_t epoch) {
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_prefix;
     __shared__ uint64_t s_w[LB_BLOCK / 64];
+    const uint32_t y = blockIdx.y;
+    const uint32_t* __restrict__ in = a.in[y];
+    uint64_t* __restrict__ out = a.out[y];
+    const uint32_t n = a.n[y], nbt = a.nb[y];
+    unsigned long long* state = state0 + (size_t)y * a.sstride;
+    unsigned long long* ctr = ctr0 + 2 * y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) s_tile = (uint32_t)atomicAdd(&ctr[0], 1ull);
     __syncthreads();
     const uint32_t tile = s_tile;
+    if (tile >= nbt) {
+        if (tid == 0 && atomicAdd(&ctr[1], 1ull) == gridDim.x - 1) {
+            ctr[0] = 0;
+            ctr[1] = 0;
+        }
+        return;
+    }
     const uint64_t i0 = (uint64_t)tile * LB_TILE + (uint64_t)tid * LB_ITEMS;
     uint32_t v[LB_ITEMS];
     if (i0 + LB_ITEMS <= n && ((uintptr_t)(in + i0) & 15) == 0) {
@@ -3347,7 +3368,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_scan_lb(const uint32_t* __restrict
             run += v[k];
         }
     }
-    if (tile == gridDim.x - 1 && tid == 0) out[n] = s_prefix + total;
+    if (tile == nbt - 1 && tid == 0) out[n] = s_prefix + total;
     if (tid == 0 && atomicAdd(&ctr[1], 1ull) == gridDim.x - 1) {
         ctr[0] = 0;
         ctr[1] = 0;
@@ -3380,9 +3401,15 @@ __global__ void k_finalize(const uint64_t* __restrict__ out_offs, const uint64_t
 // straddles pieces ORs the masked windows of each piece it touches.  Source bytes never pass through
 // LDS.  A tile with more spans than the piece table holds is assembled in several passes.  Rows of
 // any length (a whole transcript) take the same path.
-constexpr int REDACT_BLOCK = 256;
+#ifndef REDACT_BLOCK_N
+#define REDACT_BLOCK_N 256
+#endif
+constexpr int REDACT_BLOCK = REDACT_BLOCK_N;
 #ifndef REDACT_ABLATE
 #define REDACT_ABLATE 0             // measurement builds only: 1 = no assembly, 2 = tables only, 3 = no source loads
+#endif
+#ifndef REDACT_NT
+#define REDACT_NT 1                 // non-temporal output stores in the pipelined loop
 #endif
 #ifndef REDACT_PIPE
 #define REDACT_PIPE 1               // tile_assemble's pipelined interior-block loop (0: one block at a time)
@@ -3406,6 +3433,10 @@ struct RSpan {          // one kept span in batch order (16 B)
 // s_pout[total_p] = tile output length) is in LDS; a block -> piece table is built, then lane i
 // assembles aligned 16-byte output blocks i, i+blockDim, ...  Returns false (nothing written) when
 // the piece table did not fit (the caller's slow path runs instead).
+// PIPE: the pipelined interior loop (k_redact: 518 -> 506 us at config 2; the window re-scan's
+// k_win_redact, whose tiles gather ring entries, measured slower with it: 84 -> 89 us, so it keeps the
+// one-block loop)
+template <bool PIPE>
 __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint64_t* s_psrc, uint32_t total_p,
                                               uint16_t* s_bp, uint32_t* s_wsum, uint8_t* __restrict__ out,
                                               int64_t out_lo, int64_t out_hi) {
@@ -3519,7 +3550,7 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
         }
     };
 #if REDACT_PIPE
-    if (table) {
+    if (PIPE && table) {
         // Interior blocks (all 16 bytes in [out_lo, out_hi)) in a software pipeline: block q + 256's
         // piece lookup and its two source loads are issued before block q is merged and stored.  Every
         // load and store is unconditional (a chunk holding no byte of the piece is replaced by the
@@ -3563,7 +3594,11 @@ __device__ __forceinline__ void tile_assemble(const uint32_t* s_pout, const uint
             auto put = [&](const Fast& f, int64_t q) {
                 const uint4 v = window16(f.x, f.y, f.sh);
                 u32x4_t nv = {v.x, v.y, v.z, v.w};
+#if REDACT_NT
                 __builtin_nontemporal_store(nv, reinterpret_cast<u32x4_t*>(op + q));
+#else
+                *reinterpret_cast<u32x4_t*>(op + q) = nv;
+#endif
                 if (!f.one) fix |= 1u << (uint32_t)((q - q0) / REDACT_BLOCK);
             };
             Fast f0, f1;
@@ -3796,7 +3831,7 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_redact(const RulesDev R, const
         }
         __syncthreads();
 #if REDACT_ABLATE != 1
-        tile_assemble(s_pout, s_psrc, n == 0 ? 1u : 2 * n + 1, s_bp, s_wsum, out, lo, hi);
+        tile_assemble<true>(s_pout, s_psrc, n == 0 ? 1u : 2 * n + 1, s_bp, s_wsum, out, lo, hi);
 #endif
         __syncthreads();
         i += n;
@@ -4534,7 +4569,7 @@ __global__ __launch_bounds__(REDACT_BLOCK) void k_win_redact(const RulesDev R, c
     if (tid == 0 && staged) s_pout[total_p] = (uint32_t)(out_hi - out_lo);
     __syncthreads();
     if (staged) {
-        tile_assemble(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
+        tile_assemble<false>(s_pout, s_psrc, total_p, s_bp, s_wsum, out, out_lo, out_hi);
     } else {
         // one wavefront per window, byte-granular
         for (uint32_t i = wid; i < nu; i += REDACT_BLOCK / 64) {
@@ -4906,6 +4941,12 @@ struct pii_engine {
     uint64_t cap_h_ext = 0;
     uint32_t cap_h_ext_n = 0;
     hipEvent_t tev[7] = {};
+    // what a call records with HIP events (pii_set_timing): 0 = only the completion event; 1 = + the
+    // call's start and the events around k_scan / k_redact (the roofline kernels); 2 = + the stage
+    // boundaries (pii_last_timings [0..4]).  An event record between two kernels costs ~6 us of GPU
+    // time (the queue drains at the marker): level 2's five stage events were ~30 us of a config-2
+    // step and ~12% of a window re-scan step (rocprofv3 kernel trace gaps).
+    int timing = 1;
     float last_ms[6] = {};
     hipEvent_t kev[4] = {};           // around k_scan and k_redact (the roofline kernels)
     bool kev_valid = false;
@@ -5117,12 +5158,13 @@ constexpr uint32_t LB_MAX_TILES = 64;
 
 int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out, hipStream_t st,
                    const uint32_t* in2 = nullptr, uint32_t n2 = 0, uint64_t* out2 = nullptr) {
-    const uint32_t nb = (n + LB_TILE - 1) / LB_TILE;
+    const uint32_t nb = (n + LB_TILE - 1) / LB_TILE, nb2 = in2 ? (n2 + LB_TILE - 1) / LB_TILE : 0;
     if (in2 == nullptr && nb == 0) {
         HIPCHK(hipMemsetAsync(out, 0, sizeof(uint64_t), st));
         return PII_OK;
     }
-    if (in2 != nullptr || nb > LB_MAX_TILES) {
+    // (a scan of zero items still writes its total: the look-back form needs a tile for it)
+    if (nb > LB_MAX_TILES || nb2 > LB_MAX_TILES || (in2 && (nb == 0 || nb2 == 0))) {
         // reduce / scan-of-sums / apply; a second scan rides along in blockIdx.y
         ScanArgs a{{in, in2 ? in2 : in}, {out, out2 ? out2 : out}, {n, in2 ? n2 : 0u}, 0};
         const uint32_t nt = std::max<uint32_t>(1, (std::max(n, a.n[1]) + SCAN_TILE - 1) / SCAN_TILE);
@@ -5134,15 +5176,18 @@ int exclusive_scan(pii_engine* e, const uint32_t* in, uint32_t n, uint64_t* out,
         HIPCHK(hipGetLastError());
         return PII_OK;
     }
-    if (nb > e->lb_cap) {
-        int rc = grow(e, e->lb_state, (size_t)nb + 64);
+    if (std::max(nb, nb2) > e->lb_cap) {
+        const uint32_t cap = std::max(nb, nb2) + 64;
+        int rc = grow(e, e->lb_state, 2 * (size_t)cap);
         if (rc) return rc;
-        HIPCHK(hipMemsetAsync(e->lb_state, 0, ((size_t)nb + 64) * 8, st));
-        e->lb_cap = nb + 64;
+        HIPCHK(hipMemsetAsync(e->lb_state, 0, 2 * (size_t)cap * 8, st));
+        e->lb_cap = cap;
     }
     e->lb_epoch = (e->lb_epoch + 1) & 0xffffffu;
     if (e->lb_epoch == 0) e->lb_epoch = 1;
-    k_scan_lb<<<nb, LB_BLOCK, 0, st>>>(in, n, out, e->lb_state, e->lb_ticket, e->lb_epoch);
+    // a pair of small scans (a re-scan step's lane and row scans) in one launch
+    const LbArgs a{{in, in2 ? in2 : in}, {out, out2 ? out2 : out}, {n, n2}, {nb, nb2}, e->lb_cap};
+    k_scan_lb<<<dim3(std::max(nb, nb2), in2 ? 2 : 1), LB_BLOCK, 0, st>>>(a, e->lb_state, e->lb_ticket, e->lb_epoch);
     HIPCHK(hipGetLastError());
     return PII_OK;
 }
@@ -5215,7 +5260,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         HIPCHK(hipMemcpyAsync(e->d_err, err_init, 24, hipMemcpyDeviceToDevice, st));
     else
         HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));   // err, long_count, ncommit, pair_count
-    HIPCHK(hipEventRecord(e->tev[0], st));
+    if (e->timing >= 1) HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt / CI_ROWS + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
                                                                 e->long_min, R.kw_always_min, e->first_utt,
@@ -5259,7 +5304,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                     k_halo<<<row_grid(e, total_bytes), HALO_BLOCK, e->sg_lds[q], st>>>(Rq, g, text, e->long_rows,
                                                                                   e->long_count, stq, e->d_err);
                 if (q == 0) {
-                    HIPCHK(hipEventRecord(e->kev[0], st));
+                    if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[0], st));
                     if (two) {
                         HIPCHK(hipEventRecord(e->ev_fork, st));
                         for (uint32_t i = 0; i + 1 < ns_scan; ++i) HIPCHK(hipStreamWaitEvent(e->aux[i], e->ev_fork, 0));
@@ -5288,7 +5333,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                 HIPCHK(hipEventRecord(e->ev_join[i], e->aux[i]));
                 HIPCHK(hipStreamWaitEvent(st, e->ev_join[i], 0));
             }
-            HIPCHK(hipEventRecord(e->kev[1], st));
+            if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[1], st));
             if (e->long_min != NO_CUTS)
                 k_scan_fix<<<dim3(row_grid(e, total_bytes), e->n_sg), 256, e->max_sg_lds + FIX_LDS, st>>>(
                     e->d_sg, e->d_sg_lds, g, text, e->long_rows, e->long_count, e->ev, e->cap_ev, e->lane_cnt,
@@ -5323,7 +5368,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         }
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[1], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[1], st));
     const uint32_t nblk = (uint32_t)(((uint64_t)n_utt + CTX_TILE - 1) / CTX_TILE);
     if (n_utt > 0 && ctx_kernels) {
         // 16-byte row groups when the caller's arrays allow it
@@ -5336,7 +5381,7 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             e->commit, e->incl, e->ncommit, win_ctx);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[2], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[2], st));
     if (n_utt > 0 && n_chunks > 0 && pair_first) {
         (e->img_first.global ? k_pair_first<true> : k_pair_first<false>)<<<e->n_seg, PAIR_BLOCK,
                                                                             e->img_first.global
@@ -5445,10 +5490,10 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                                           e->d_err);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[3], st));
-    // row output offsets and per-lane span offsets: one dual scan for a big batch (3 launches instead
-    // of 6), two single-pass look-back scans for a small one
-    if (n_chunks > 0 && (n_utt + LB_TILE - 1) / LB_TILE > LB_MAX_TILES) {
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[3], st));
+    // row output offsets and per-lane span offsets: one dual scan (a big batch: 3 launches instead of
+    // 6; a small one: one single-pass look-back launch instead of 2)
+    if (n_chunks > 0) {
         if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st, e->lane_nf, n_chunks, e->lane_sp))) return rc;
     } else {
         if ((rc = exclusive_scan(e, e->out_len, n_utt, out_offs, st))) return rc;
@@ -5457,7 +5502,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
     k_finalize<<<1, 1, 0, st>>>(out_offs, e->lane_sp, n_utt, n_chunks, out_cap, span_cap, e->d_err, e->d_totals,
                                 pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, nullptr);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e->tev[4], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
         if (n_chunks > 0) {
             const uint32_t nsb = (n_chunks + 255) / 256;
@@ -5467,10 +5512,10 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             k_tile_first<<<(tiles + 255) / 256, 256, 0, st>>>(R, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
                                                               (uint32_t)((uintptr_t)out & 15), tiles, e->d_err,
                                                               e->tile_first);
-            HIPCHK(hipEventRecord(e->kev[2], st));
+            if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[2], st));
             k_redact<<<tiles, REDACT_BLOCK, 0, st>>>(R, text, offs, e->rsp, e->lane_sp + n_chunks, out_offs + n_utt,
                                                      total_bytes, e->tile_first, e->d_err, out);
-            HIPCHK(hipEventRecord(e->kev[3], st));
+            if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[3], st));
             if (!wf)        // (window findings are not counted, as on the incremental window path)
                 k_hist_reduce<<<dim3(e->hist_types, std::max(1u, std::min(32u, nsb / 256))), 256, 0, st>>>(
                     e->hist_part, nsb, (int)e->hist_types, e->d_err, e->hist);
@@ -5486,7 +5531,7 @@ int run_pipeline(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
         }
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[5], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[5], st));
     HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, hist_bytes(e), hipMemcpyDeviceToHost, st));
     e->h_hist_valid = true;
     HIPCHK(hipEventRecord(e->tev[6], st));
@@ -5669,7 +5714,7 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     if (n_utt > 0 && n_chunks > 0)
         (e->img_eval.global ? k_win_halo<true> : k_win_halo<false>)<<<nb, 256, e->img_eval.lds(), st>>>(
             e->img_eval.d, e->img_eval.li, W, B, e->wc, e->d_err);
-    HIPCHK(hipEventRecord(e->tev[3], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[3], st));
     if (n_utt > 0) {
         k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
         if ((rc = exclusive_scan(e, e->wbound, n_utt, e->wfbase, st))) return rc;
@@ -5678,24 +5723,28 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
                                                              e->wfd_cap, e->wfd, e->n_wfind, e->wout_len, e->d_err);
         HIPCHK(hipGetLastError());
     }
-    if ((rc = exclusive_scan(e, e->wout_len, n_utt, out_offs, st))) return rc;
-    if ((rc = exclusive_scan(e, e->n_wfind, n_utt, e->wspan_offs, st))) return rc;
+    if (n_utt > 0) {
+        if ((rc = exclusive_scan(e, e->wout_len, n_utt, out_offs, st, e->n_wfind, n_utt, e->wspan_offs))) return rc;
+    } else {
+        if ((rc = exclusive_scan(e, e->wout_len, n_utt, out_offs, st))) return rc;
+        if ((rc = exclusive_scan(e, e->n_wfind, n_utt, e->wspan_offs, st))) return rc;
+    }
     if (n_utt > 0) k_win_alloc<<<nb, 256, 0, st>>>(W, B, e->wnew, e->d_err);
     k_finalize<<<1, 1, 0, st>>>(out_offs, e->wspan_offs, n_utt, n_utt, out_cap, span_cap, e->d_err, e->d_totals,
                                 pcount, n_chunks > 0 ? e->lane_ev + n_chunks : nullptr, n_utt > 0 ? e->wfbase + n_utt : nullptr);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e->tev[4], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0) {
-        HIPCHK(hipEventRecord(e->kev[2], st));
+        if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[2], st));
         k_win_redact<<<(n_utt + WIN_TILE - 1) / WIN_TILE, REDACT_BLOCK, 0, st>>>(
             R, W, B, e->wfd, e->wfbase, e->n_wfind, out_offs, e->wspan_offs, e->d_err, out, spans);
-        HIPCHK(hipEventRecord(e->kev[3], st));
+        if (e->timing >= 1) HIPCHK(hipEventRecord(e->kev[3], st));
         k_win_commit<<<(uint32_t)(((uint64_t)n_utt * 16 + 255) / 256), 256, 0, st>>>(W, B, e->wnew, e->d_err);
         k_ctx_commit<<<std::min<uint32_t>(nb, 4 * e->n_cu), 256, 0, st>>>(slot, e->kw, ts, e->incl, e->ncommit,
                                                                           e->commit, e->d_err, e->st_group, e->st_ts);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(e->tev[5], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[5], st));
     HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, hist_bytes(e), hipMemcpyDeviceToHost, st));
     e->h_hist_valid = true;
     HIPCHK(hipEventRecord(e->tev[6], st));
@@ -5726,14 +5775,14 @@ int run_context(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32
     if ((rc = launch_front(e, text, offs, n_utt, n_chunks, 0, total_bytes, slot, role, ts, ctx_info, nullptr, pcount,
                            st, nullptr, true, false)))
         return rc;
-    HIPCHK(hipEventRecord(e->tev[3], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[3], st));
     k_ctx_totals<<<1, 1, 0, st>>>(e->d_err, e->d_totals);
-    HIPCHK(hipEventRecord(e->tev[4], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[4], st));
     if (n_utt > 0)
         k_ctx_commit<<<std::min<uint32_t>((n_utt + 255) / 256, 4 * e->n_cu), 256, 0, st>>>(
             slot, e->kw, ts, e->incl, e->ncommit, e->commit, e->d_err, e->st_group, e->st_ts);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e->tev[5], st));
+    if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[5], st));
     HIPCHK(hipMemcpyAsync(e->h_totals, e->d_totals, 64, hipMemcpyDeviceToHost, st));
     e->h_hist_valid = false;
     HIPCHK(hipEventRecord(e->tev[6], st));
@@ -6261,6 +6310,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("hipMalloc failed");
     }
     if (const char* v = std::getenv("PII_SCAN2")) e->scan2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PII_TIMING")) e->timing = std::max(0, std::min(2, std::atoi(v)));
     if (max_lds > 64 * 1024 &&
         (hipFuncSetAttribute((const void*)k_scan2<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=
              hipSuccess ||
@@ -6303,8 +6353,8 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
     if (hipMalloc(&e->st_group, ns * 4) != hipSuccess || hipMalloc(&e->st_ts, ns * 8) != hipSuccess ||
         hipMalloc(&e->stamp, ns * 4) != hipSuccess ||
         hipMalloc(&e->d_err, 64) != hipSuccess || hipMalloc(&e->d_totals, hist_bytes(e)) != hipSuccess ||
-        hipMalloc(&e->lb_ticket, 16) != hipSuccess ||
-        hipMemset(e->lb_ticket, 0, 16) != hipSuccess)
+        hipMalloc(&e->lb_ticket, 32) != hipSuccess ||
+        hipMemset(e->lb_ticket, 0, 32) != hipSuccess)
         return fail("state allocation failed");
     e->long_count = e->d_err + 1;
     e->ncommit = e->d_err + 2;
@@ -6413,9 +6463,9 @@ int pii_reserve(pii_engine* e, uint32_t max_utt, uint64_t max_bytes, uint64_t ma
     if ((rc = ensure_scratch(e, max_utt, max_bytes, (uint32_t)std::min<uint64_t>(lanes, 0xffffffffull))) ||
         (rc = ensure_queues(e, max_bytes)) || (rc = ensure_redact(e, max_spans, max_out)))
         return rc;
-    if (e->lb_cap < LB_MAX_TILES + 64) {      // the look-back scan's tile states (exclusive_scan)
-        if ((rc = grow(e, e->lb_state, (size_t)LB_MAX_TILES + 64))) return rc;
-        HIPCHK(hipMemsetAsync(e->lb_state, 0, ((size_t)LB_MAX_TILES + 64) * 8, e->stream));
+    if (e->lb_cap < LB_MAX_TILES + 64) {      // the look-back scans' tile states (exclusive_scan: two scans)
+        if ((rc = grow(e, e->lb_state, 2 * ((size_t)LB_MAX_TILES + 64)))) return rc;
+        HIPCHK(hipMemsetAsync(e->lb_state, 0, 2 * ((size_t)LB_MAX_TILES + 64) * 8, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         e->lb_cap = LB_MAX_TILES + 64;
     }
@@ -6447,13 +6497,15 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
     float tot = 0;
     for (int i = 0; i < 5; ++i) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
+        if (e->timing >= 2) HIPCHK(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
         e->last_ms[i] = ms;
         tot += ms;
     }
+    // (level 1: the call from its start to its completion event, the totals' copy included)
+    if (e->timing == 1) HIPCHK(hipEventElapsedTime(&tot, e->tev[0], e->tev[6]));
     e->last_ms[5] = tot;
     e->last_kms[0] = e->last_kms[1] = 0.f;
-    if (e->kev_valid) {
+    if (e->kev_valid && e->timing >= 1) {
         HIPCHK(hipEventElapsedTime(&e->last_kms[0], e->kev[0], e->kev[1]));
         HIPCHK(hipEventElapsedTime(&e->last_kms[1], e->kev[2], e->kev[3]));
     }
@@ -6484,6 +6536,13 @@ int pii_sync(pii_engine* e, uint64_t totals[3]) {
         return PII_E_DEVICE;
     }
     if (f & ERR_CAPACITY) return PII_E_CAPACITY;
+    return PII_OK;
+}
+
+int pii_set_timing(pii_engine* e, int level) {
+    if (!e || level < 0 || level > 2) return PII_E_ARG;
+    HIPCHK(hipStreamSynchronize(e->stream));      // (no call in flight records under the old level)
+    e->timing = level;
     return PII_OK;
 }
 

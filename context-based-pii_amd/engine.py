@@ -28,7 +28,7 @@ EXPORTS = ["pii_engine_create", "pii_engine_destroy", "pii_engine_info", "pii_ty
            "pii_window_count", "pii_rescan_window", "pii_rescan_window_device",
            "pii_rescan_window_device_ex", "pii_scan_redact_ext", "pii_scan_redact_device_ext", "pii_window_enable_ex",
            "pii_window_mode", "pii_set_scratch_limit", "pii_scratch_bytes", "pii_context_resize",
-           "pii_context_update"]
+           "pii_context_update", "pii_set_timing"]
 PII_WINDOW_FULL = 1
 
 
@@ -96,6 +96,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pii_context_update.argtypes = [P, P, P, c.c_uint32, P, P, P, P]
     lib.pii_histogram.argtypes = [P, U64, c.c_uint32]
     lib.pii_histogram_reset.argtypes = [P]
+    lib.pii_set_timing.argtypes = [P, c.c_int]
     lib.pii_last_timings.argtypes = [P, c.POINTER(c.c_float)]
     lib.pii_last_timings_ex.argtypes = [P, c.POINTER(c.c_float), c.c_uint32]
     lib.pii_last_queue_sizes.argtypes = [P, U64, U64]
@@ -346,6 +347,13 @@ class Engine:
         if rc != PII_OK:
             raise self._err(rc, "pii_sync")
         return int(tot[0]), int(tot[1]), int(tot[2])
+
+    def set_timing(self, level: int) -> None:
+        """HIP events a call records: 0 completion only, 1 (default) + start and the roofline kernels,
+        2 + the stage boundaries (pii_set_timing; each event costs the stream a few microseconds)."""
+        rc = self.lib.pii_set_timing(self.h, int(level))
+        if rc:
+            raise self._err(rc, "pii_set_timing")
 
     def timings(self) -> List[float]:
         ms = (ctypes.c_float * 6)()

@@ -189,8 +189,14 @@ int pii_context_update(struct pii_engine* e, const uint8_t* bytes, const uint64_
 int pii_histogram(struct pii_engine* e, uint64_t* counts, uint32_t n);
 int pii_histogram_reset(struct pii_engine* e);
 
-/* per-kernel device time of the last call, milliseconds (HIP events on the engine stream):
- * [0] scan [1] context [2] resolve [3] offsets [4] redact [5] total */
+/* what a call records with HIP events on its stream: 0 = its completion only; 1 (default) = + its
+ * start and the events around the scan and redaction kernels; 2 = + the stage boundaries.  An event
+ * between two kernels costs the stream a few microseconds, so level 2 is for profiling runs.
+ * (env PII_TIMING sets the default; the call waits for the engine stream) */
+int pii_set_timing(struct pii_engine* e, int level);
+/* per-stage device time of the last call, milliseconds (HIP events on the engine stream):
+ * [0] scan [1] context [2] resolve [3] offsets [4] redact (timing level 2; 0 below) [5] total
+ * (level >= 1) */
 int pii_last_timings(struct pii_engine* e, float ms[6]);
 /* the same six, then [6] the reverse DFA scan kernel (k_scan) and [7] the redaction kernel
  * (k_redact) alone; fills min(n, 8) entries and returns that count */
