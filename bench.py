@@ -1218,6 +1218,7 @@ def window_main(args):
     per_stage /= K
     k_red /= K
     stages = stage_probe(eng, lambda i: step(warm + K + i)) if warm + K + 3 <= U else per_stage
+    wkey = "window_config5" if c5path else "window"          # (profiles/traffic.json: its own PMC passes)
     # window bytes read to write the outputs: every window's utterances and separators
     lens = (meta.offsets[1:] - meta.offsets[:-1]).astype(np.int64).reshape(U, C)
     win_in = 0
@@ -1250,13 +1251,14 @@ def window_main(args):
         "stages_ms": {k: round(float(v), 4) for k, v in zip(
             ["scan+pairs", "context", "first+cands", "select+offsets", "redact+commit", "pipeline"], stages)},
         "stages_note": STAGES_NOTE,
+        "probe_steps": 3 if warm + K + 3 <= U else 0,
         "pipeline": {"algorithmic_bytes": int(B / K), "GBps": round(B / t_pipe / 1e9, 1),
                      "frac": round(B / t_pipe / 1e9 / HBM_PEAK_GBPS, 4),
-                     "traffic": measured_pipeline_traffic(int(meta.offsets[-1]), "window")},
+                     "traffic": measured_pipeline_traffic(int(meta.offsets[-1]), wkey)},
         "roofline": {"bound": "hbm", "kernel": "k_win_redact", "achieved": round(red_B / K / (k_red / 1e3) / 1e9, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(red_B / K / (k_red / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "traffic": measured_traffic("k_win_redact", int(meta.offsets[-1]), "window"),
+                     "traffic": measured_traffic("k_win_redact", int(meta.offsets[-1]), wkey),
                      "algorithmic_bytes": int(red_B / K), "launch_ms": round(k_red, 4)},
         "cpu_baseline": cpu,
     }

@@ -6256,6 +6256,15 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
                     hipSuccess)
                 return fail("cannot raise the LDS limit of a pair kernel");
+        if (const char* v = std::getenv("PII_VERBOSE"); v && std::atoi(v) > 0) {
+            const std::pair<const char*, const DevImage*> ims[] = {
+                {"first", &e->img_first}, {"first_hot", &e->img_first_hot}, {"eval", &e->img_eval},
+                {"eval_rg", &e->img_eval_rg}, {"sel", &e->img_sel}, {"sel_rg", &e->img_sel_rg}, {"wsel", &e->img_wsel}};
+            for (auto& im : ims)
+                if (im.second->d)
+                    std::fprintf(stderr, "pii: image %-9s %8u bytes %s\n", im.first, im.second->li.total,
+                                 im.second->global ? "global" : "lds");
+        }
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             e->n_cu = prop.multiProcessorCount;

@@ -14,7 +14,7 @@ for W in scan config5 window; do
   cp "$S/prof_$W/run_kernel_stats.csv" "$DEST/kernel_stats_$W.csv"
   python3 tools/pmc_bound.py "$S/bound_$W" --json "$DEST/bound_$W.json" > "$DEST/bound_$W.txt"
 done
-for W in scan config5 window long; do
+for W in scan config5 window long window_config5; do
   python3 tools/pmc_traffic.py "$S/traffic_$W" --workload "$W" > "$DEST/traffic_$W.json"
 done
 echo "collected $S -> $DEST"

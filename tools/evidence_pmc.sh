@@ -16,6 +16,9 @@ for W in scan config5 window long; do
   bash tools/pmc_traffic.sh "gpurun_out/$TAG/traffic_$W" "$W" --steps 2 --warmup 1 --no-cpu-baseline > "$O/traffic_$W.log" 2>&1 || { echo "PMC $W FAILED"; tail -5 "$O/traffic_$W.log"; exit 1; }
   echo "PMC $W ok"
 done
+# the window re-scan under the config-5 rules (its bench line's traffic field)
+bash tools/pmc_traffic.sh "gpurun_out/$TAG/traffic_window_config5" window --window-rules config5 --conversations 50000 --steps 2 --warmup 1 --no-cpu-baseline > "$O/traffic_window_config5.log" 2>&1 || { echo "PMC window_config5 FAILED"; tail -5 "$O/traffic_window_config5.log"; exit 1; }
+echo "PMC window_config5 ok"
 # bound / occupancy passes (wave-cycle split, achieved waves per SIMD) of every k_scan instantiation:
 # config 2 (group 0), config 5 (narrow and WIDE groups), the window step
 for W in scan config5 window; do

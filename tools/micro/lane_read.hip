@@ -72,6 +72,34 @@ __global__ __launch_bounds__(256) void k_stream4(const uint32_t* __restrict__ p,
     k_stream<uint32_t>(p, n, out);
 }
 
+// (e) per-lane forward walks of short runs of 16-byte records, the runs of neighbouring lanes adjacent
+//     (k_select's SelRec walk over a lane's matched pairs: ~6 records per lane, one-ahead prefetch)
+__global__ __launch_bounds__(256) void k_walk16(const uint4* __restrict__ p, uint64_t recs_per_lane, uint64_t n_lanes,
+                                                uint32_t* __restrict__ out) {
+    const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (c >= n_lanes) return;
+    const uint64_t r0 = c * recs_per_lane, r1 = r0 + recs_per_lane;
+    uint32_t acc = 0;
+    uint4 nx = p[r0];
+    for (uint64_t r = r0; r < r1; ++r) {
+        const uint4 w = nx;
+        if (r + 1 < r1) nx = p[r + 1];
+        acc ^= w.x ^ w.y ^ w.z ^ w.w;
+    }
+    out[c] = acc;
+}
+
+// (f) 16-byte records in a scattered order, every record once (a multiplicative permutation: the
+//     sparse kernels' gathers of event / pair records and text windows)
+__global__ __launch_bounds__(256) void k_gather16(const uint4* __restrict__ p, uint64_t n16, uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 w = p[(i * 2654435761ull) % n16];
+        acc ^= w.x ^ w.y ^ w.z ^ w.w;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 int main() {
     const uint64_t bytes = 1200ull << 20;
     uint4* d;
@@ -124,5 +152,30 @@ int main() {
         }
         printf("stream %d B/lane: %.3f ms  %.0f GB/s\n", w, best, bytes / best / 1e6);
     }
+    {
+        const uint64_t rpl = 6, lanes = bytes / 16 / rpl;
+        best = 1e9;
+        for (int it = 0; it < 6; ++it) {
+            (void)hipEventRecord(a);
+            k_walk16<<<(lanes + 255) / 256, 256>>>(d, rpl, lanes, o);
+            (void)hipEventRecord(b);
+            (void)hipEventSynchronize(b);
+            float ms;
+            (void)hipEventElapsedTime(&ms, a, b);
+            if (it) best = ms < best ? ms : best;
+        }
+        printf("walk16 (6 records/lane): %.3f ms  %.0f GB/s\n", best, lanes * rpl * 16 / best / 1e6);
+    }
+    best = 1e9;
+    for (int it = 0; it < 6; ++it) {
+        (void)hipEventRecord(a);
+        k_gather16<<<256 * 8, 256>>>(d, bytes / 16, o);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        if (it) best = ms < best ? ms : best;
+    }
+    printf("gather16: %.3f ms  %.0f GB/s\n", best, bytes / best / 1e6);
     return 0;
 }

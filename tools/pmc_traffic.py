@@ -10,6 +10,12 @@ dispatch in four patterns, and each gives its own correction (bytes read / FETCH
   stream16  k_coalesced  16 B per lane, consecutive (k_redact's text reads and tile stores' sources)
   stream8   k_stream8    8 B per lane (the scan events, pair records: the queue kernels' main loads)
   stream4   k_stream4    4 B per lane (offsets / counts / per-lane scalars)
+  walk16    k_walk16     per-lane forward walks of 6 16-byte records, neighbouring lanes adjacent
+                         (k_select's SelRec walk over each lane's matched pairs; round 6)
+  gather16  k_gather16   16-byte records in a scattered order (k_pair_first / k_pair_eval: pair and
+                         event records and text windows gathered per pair; round 6).  Its FETCH_SIZE is
+                         4x the record bytes: each record costs a 64-byte line (CALIB_LINE_MULT), so the
+                         correction is taken against the line bytes (~1.0), not the useful bytes
 Every engine kernel is assigned the pattern of its dominant read stream (KERNEL_PATTERN), and its
 hbm_bytes = FETCH_SIZE x that pattern's correction + WRITE_SIZE.  (one global factor,
 calibrated on k_scan's pattern, under-counted k_redact's coalesced stream.)  Where the bench line
@@ -33,12 +39,19 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ["context-based-pii_amd/csrc/pii_engine.hip", "context-based-pii_amd/csrc/pii_device.h"]
 CALIB_BYTES = 1200 * (1 << 20)
-CALIB_KERNELS = {"lane_rev": "k_lane_rev", "stream16": "k_coalesced", "stream8": "k_stream8", "stream4": "k_stream4"}
+CALIB_KERNELS = {"lane_rev": "k_lane_rev", "stream16": "k_coalesced", "stream8": "k_stream8", "stream4": "k_stream4",
+                 "walk16": "k_walk16", "gather16": "k_gather16"}
+# HBM bytes one calibration launch really moves, as a multiple of the bytes it reads: a scattered 16-byte
+# gather brings a whole 64-byte line per record (its FETCH_SIZE reads 4x the record bytes: the counter is
+# right at 64-byte requests, and the line's unused 48 bytes are real HBM traffic), so its correction is
+# taken against the line bytes, not the record bytes.  Every other pattern reads each byte of its lines.
+CALIB_LINE_MULT = {"gather16": 4}
 # dominant read stream per engine kernel (name prefix); anything else: stream8
 KERNEL_PATTERN = {"k_scan": "lane_rev", "k_scan_fix": "lane_rev", "k_redact": "stream16", "k_win_redact": "stream16",
                   "k_win_join": "stream16", "k_lane_bits": "stream8", "k_chunk_index": "stream8",
-                  "k_pairs_flat": "stream8", "k_pairs_merge": "stream8", "k_pair_first": "stream8",
-                  "k_pair_eval": "stream8", "k_select": "stream8", "k_spans": "stream8", "k_ctx_scan": "stream4",
+                  "k_pairs_flat": "stream8", "k_pairs_merge": "stream8", "k_pair_first": "gather16",
+                  "k_pair_eval": "gather16", "k_select": "walk16", "k_sel_fix": "walk16", "k_spans": "stream8",
+                  "k_ctx_scan": "stream4",
                   "k_ctx_apply": "stream4", "k_ctx_commit": "stream4", "k_lane_count": "stream4",
                   "k_lane_place": "stream4", "k_scan_reduce": "stream4", "k_scan_apply": "stream4",
                   "k_scan_blocks": "stream4", "k_scan_lb": "stream4", "k_tile_first": "stream8",
@@ -129,12 +142,12 @@ def main():
     if bench and w.startswith("window"):
         # only the timed steps: the bench's warm-up fills the windows (warmup >= N)
         K, W0 = int(bench[-1]["steps"]), int(bench[-1]["warmup"])
-        tail = (K, K + W0)
+        tail = (K, K + W0 + int(bench[-1].get("probe_steps", 0)))     # (+ the stage probe's calls)
     fetch = per_kernel(os.path.join(d, "fetch"), "FETCH_SIZE", tail)
     write = per_kernel(os.path.join(d, "write"), "WRITE_SIZE", tail)
     calib = per_kernel(os.path.join(d, "calib"), "FETCH_SIZE")
     # every lane_read launch reads CALIB_BYTES (k_lane_rev at 512/1024/2048 B per lane, the streams)
-    corrs = {pat: (CALIB_BYTES / (mean(calib[k]) * 1024) if calib.get(k) else None)
+    corrs = {pat: (CALIB_BYTES * CALIB_LINE_MULT.get(pat, 1) / (mean(calib[k]) * 1024) if calib.get(k) else None)
              for pat, k in CALIB_KERNELS.items()}
     corr = corrs["lane_rev"]
     cfg = bench[-1]["config"] if bench else {}
@@ -154,7 +167,7 @@ def main():
         f = mean(fetch.get(k, [0])) * 1024
         wr = mean(write.get(k, [0])) * 1024
         pat = pattern_of(k)
-        c = corrs.get(pat)
+        c = corrs.get(pat) or corrs.get("stream8")        # (an older calibration run: no walk / gather)
         e = {"fetch_reported_bytes": round(f), "write_bytes": round(wr), "fetch_pattern": pat,
              "hbm_bytes": round(f * c + wr) if c else None}
         ab = algorithmic_bytes(k, b)
