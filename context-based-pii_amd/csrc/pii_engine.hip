@@ -3873,6 +3873,9 @@ constexpr int WN_MAX = 8;          // largest window (utterances)
 constexpr int WIN_TILE = 64;       // windows per k_win_redact workgroup
 
 constexpr int WHOT_BITS = 16;      // hotword rules whose proximity results are kept resident
+#ifndef WIN_HALO_ABLATE
+#define WIN_HALO_ABLATE 0           // measurement builds only: 1 = no hotword DFA runs, 2 = row prologue only
+#endif
 struct WCand {          // one resident candidate (16 B)
     uint32_t s, e;      // match [s, e), relative to its utterance
     uint16_t p;         // detector pattern (any rule set: config 5 has 544)
@@ -3987,6 +3990,42 @@ __device__ bool hot_run_win(const Pool& pool, const int32_t* d, const WinRing& W
         sl = sh + 1;
     }
     return (tr[st * nc + nc - 1] & 0x4000u) != 0;
+}
+
+// hot_span over text[lo, hi) with every chunk of a short window (<= 64 bytes) loaded before the first
+// step (hot_span loads the next 16 bytes only after stepping the current ones)
+__device__ __forceinline__ bool hot_span_pre(const uint16_t* tr, const uint8_t* cm, uint32_t nc, const uint8_t* text,
+                                             int lo, int hi, uint32_t& st) {
+    if (hi - lo > 64) return hot_span(tr, cm, nc, text, lo, hi, st);
+    uint4 w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j = lo + 16 * c;
+        w[c] = make_uint4(0, 0, 0, 0);
+        if (j < hi) w[c] = load16(text + j, 0, hi - j < 16 ? hi - j : 16);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j = lo + 16 * c;
+        if (j >= hi) break;
+        const int n = hi - j < 16 ? hi - j : 16;
+        uint4 x = w[c];
+#pragma unroll 1
+        for (int g = 0; g < n; g += 4) {
+            const uint32_t v = x.x;
+            const uint32_t cl[4] = {cm[v & 0xffu], cm[(v >> 8) & 0xffu], cm[(v >> 16) & 0xffu], cm[v >> 24]};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (g + k < n) {
+                    const uint32_t e = tr[st * nc + cl[k]];
+                    if (e & 0x4000u) return true;
+                    st = e & DFA_STATE_MASK;
+                }
+            }
+            x = make_uint4(x.y, x.z, x.w, 0u);
+        }
+    }
+    return false;
 }
 
 // per matched pair: validator + every hotword rule the pattern's type has in ANY context variant,
@@ -4186,10 +4225,45 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
 // utterances are evaluated ONCE, here, over the predecessors the row's own window holds (those are
 // the only ones any later window can hold before it): hotx + need.  A later window in which the
 // utterance has j >= need predecessors reuses hotx; j == 0 (window start) reuses hot.
+// Two phases per workgroup of HALO_ROWS rows.  Phase 1, a thread per row: the row's window entries
+// (text, length, counted back from the row) into LDS, need written, and one ITEM per (candidate,
+// hotword rule) whose before-window must be re-run, appended to the workgroup's LDS list.  Phase 2:
+// the items spread over all threads, one DFA run each, hits ORed into hotx.  (One thread running all
+// of its row's items: a wavefront took as long as its busiest row's candidates x rules x window
+// steps, 83 us per config-3 step at 0.8 waves / SIMD; two threads per row: 49 us.)
+constexpr int HALO_ROWS = 256, HALO_ITEMS = 1024;
+constexpr uint32_t HALO_LDS = HALO_ROWS * WN_MAX * 12 + HALO_ROWS * 12 + HALO_ITEMS * 8 + 16;
+
+// hot_run_win over a row's LDS window table (rt / rl: the entries counted back from the row, 0 = the
+// row itself, j = the oldest)
+__device__ __forceinline__ bool hot_run_back(const Pool& pool, const int32_t* d, const uint64_t* rt, const uint32_t* rl,
+                                             int j, uint32_t lo, uint32_t hi) {
+    const uint16_t* tr = pool.trans + d[0];
+    const uint8_t* cm = pool.cmap + d[2];
+    const uint32_t nc = (uint32_t)d[3];
+    uint32_t st = (uint32_t)d[4];
+    uint32_t sl = 0;
+    for (int i = j; i >= 0; --i) {
+        const uint32_t sh = sl + rl[i];
+        if (sh >= lo) {
+            if (sl >= hi) break;
+            const int a = (int)(max(lo, sl) - sl), b = (int)(min(hi, sh) - sl);
+            if (hot_span_pre(tr, cm, nc, reinterpret_cast<const uint8_t*>(rt[i]), a, b, st)) return true;
+            if (i > 0 && sh < hi) {
+                const uint32_t x = tr[st * nc + cm['\n']];
+                if (x & 0x4000u) return true;
+                st = x & DFA_STATE_MASK;
+            }
+        }
+        sl = sh + 1;
+    }
+    return (tr[st * nc + nc - 1] & 0x4000u) != 0;
+}
+
 template <bool GI>
-__global__ __launch_bounds__(256) void k_win_halo(const uint4* __restrict__ img, const LdsImage li, const WinRing W,
-                                                  const WinBatch B, WCand* __restrict__ wc,
-                                                  const uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(HALO_ROWS) void k_win_halo(const uint4* __restrict__ img, const LdsImage li, const WinRing W,
+                                                        const WinBatch B, WCand* __restrict__ wc, uint32_t item_cap,
+                                                        const uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds4[];
     if (*err & (ERR_ABORT | ERR_SLOT)) return;
     const uint8_t* lb = load_image<GI>(img, li.total, lds4);
@@ -4198,40 +4272,77 @@ __global__ __launch_bounds__(256) void k_win_halo(const uint4* __restrict__ img,
     const int32_t* hrule = reinterpret_cast<const int32_t*>(lb + li.off[EV_HRULE]);
     const uint16_t* dtype = reinterpret_cast<const uint16_t*>(lb + li.off[EV_DTYPE]);
     const uint32_t* thot = reinterpret_cast<const uint32_t*>(lb + li.off[EV_THOT]);
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= B.n_utt) return;
-    const uint32_t nc = B.wc_n[u];
-    if (nc == 0) return;
-    const WinIt it = win_begin(W, B, u);
+    // item_cap <= HALO_ITEMS (smaller only in tests: PII_HALO_ITEMS, the list-full path)
+    // the tables after the image (dynamic LDS: image bytes rounded up to 16, then HALO_LDS)
+    uint8_t* hb0 = reinterpret_cast<uint8_t*>(lds4) + (GI ? 0u : (li.total + 15u) & ~15u);
+    uint64_t* s_rt = reinterpret_cast<uint64_t*>(hb0);                            // [row][WN_MAX]
+    uint32_t* s_rl = reinterpret_cast<uint32_t*>(s_rt + HALO_ROWS * WN_MAX);       // [row][WN_MAX]
+    uint64_t* s_cl = reinterpret_cast<uint64_t*>(s_rl + HALO_ROWS * WN_MAX);       // [row]: its candidates
+    uint32_t* s_j = reinterpret_cast<uint32_t*>(s_cl + HALO_ROWS);                 // [row]: predecessors
+    uint2* s_item = reinterpret_cast<uint2*>(s_j + HALO_ROWS);                     // (ps, row << 24 | k << 4 | rule)
+    uint32_t* s_n = reinterpret_cast<uint32_t*>(s_item + HALO_ITEMS);
+    const int tid = threadIdx.x;
+    if (tid == 0) *s_n = 0;
+    __syncthreads();
+    const uint32_t u = blockIdx.x * HALO_ROWS + tid;
+    const uint32_t nc = u < B.n_utt ? B.wc_n[u] : 0u;
+    WinIt it;
+    it.nw = 1;
+    if (nc) it = win_begin(W, B, u);
     const int j = it.nw - 1;                       // predecessors available
-    if (j == 0) return;
-    WCand* cl = wc + B.wc_first[u];
-    uint32_t oj = 0;                                // window offset of row u
-    for (int q = 0; q < j; ++q) oj += win_at(W, B, it, q).len + 1;
-    for (uint32_t k = 0; k < nc; ++k) {
-        WCand C = cl[k];
-        uint32_t mask = thot[dtype[C.p]] & ((1u << WHOT_BITS) - 1);
-        int wbmax = 0;
-        for (uint32_t m = mask; m; m &= m - 1) wbmax = max(wbmax, hrule[4 * __builtin_ctz(m)]);
-        if ((int)C.s >= wbmax) continue;
-        // predecessors the longest before-window reaches (all available ones if it reaches past them)
-        int need = 0;
-        uint32_t cover = C.s;
-        while (need < j && cover < (uint32_t)wbmax) {
-            ++need;
-            cover += win_at(W, B, it, j - need).len + 1;
+    if (nc && j > 0) {
+        WCand* cl = wc + B.wc_first[u];
+        uint64_t* rt = s_rt + tid * WN_MAX;
+        uint32_t* rl = s_rl + tid * WN_MAX;
+        uint32_t oj = 0;                            // window offset of row u
+        for (int i = 0; i <= j; ++i) {
+            const WEntry E = win_at(W, B, it, j - i);
+            rt[i] = (uint64_t)(uintptr_t)E.t;
+            rl[i] = E.len;
+            if (i >= 1) oj += E.len + 1;
         }
-        uint32_t hx = C.hot;
-        const uint32_t ps = oj + C.s;
-        for (uint32_t m = mask & ~(uint32_t)C.hot; m; m &= m - 1) {
-            const int h = __builtin_ctz(m);
-            const int wb = hrule[4 * h];
-            if (wb > 0 && (int)C.s < wb && hot_run_win(pool, hdesc + 8 * h, W, B, it, ps > (uint32_t)wb ? ps - wb : 0u, ps))
-                hx |= 1u << h;
+        s_cl[tid] = (uint64_t)(uintptr_t)cl;
+        s_j[tid] = (uint32_t)j;
+        for (uint32_t k = 0; k < nc; ++k) {
+            const WCand C = cl[k];
+            const uint32_t mask = thot[dtype[C.p]] & ((1u << WHOT_BITS) - 1);
+            int wbmax = 0;
+            for (uint32_t m = mask; m; m &= m - 1) wbmax = max(wbmax, hrule[4 * __builtin_ctz(m)]);
+            if ((int)C.s >= wbmax) continue;
+            // predecessors the longest before-window reaches (all available ones if it reaches past them)
+            int need = 0;
+            uint32_t cover = C.s;
+            while (need < j && cover < (uint32_t)wbmax) {
+                ++need;
+                cover += rl[need] + 1;
+            }
+            cl[k].need = (uint8_t)need;
+            const uint32_t ps = oj + C.s;
+            uint32_t hx = 0;
+            for (uint32_t m = mask & ~(uint32_t)C.hot; m; m &= m - 1) {
+                const uint32_t hb = (uint32_t)__builtin_ctz(m);
+                const int wb = hrule[4 * hb];
+                if (wb <= 0 || (int)C.s >= wb) continue;
+                const uint32_t q = atomicAdd(s_n, 1u);
+                if (q < item_cap && k < (1u << 20)) {
+                    s_item[q] = make_uint2(ps, (uint32_t)tid << 24 | k << 4 | hb);
+                } else if (hot_run_back(pool, hdesc + 8 * hb, rt, rl, j, ps > (uint32_t)wb ? ps - wb : 0u, ps)) {
+                    hx |= 1u << hb;                 // (list full: run here)
+                }
+            }
+            if (hx) atomicOr(reinterpret_cast<uint32_t*>(cl + k) + 3, hx << 16);   // hotx (dword 3: hot | hotx << 16)
         }
-        C.need = (uint8_t)need;
-        C.hotx = (uint16_t)hx;
-        cl[k] = C;
+    }
+    __syncthreads();
+    const uint32_t n = min(*s_n, item_cap);
+    for (uint32_t q = tid; q < n; q += HALO_ROWS) {
+        const uint2 I = s_item[q];
+        const uint32_t r = I.y >> 24, k = (I.y >> 4) & 0xfffffu, hb = I.y & 15u;
+        const uint32_t ps = I.x, wb = (uint32_t)hrule[4 * hb];
+        if (hot_run_back(pool, hdesc + 8 * hb, s_rt + r * WN_MAX, s_rl + r * WN_MAX, (int)s_j[r], ps > wb ? ps - wb : 0u, ps)) {
+            WCand* C = reinterpret_cast<WCand*>((uintptr_t)s_cl[r]) + k;
+            atomicOr(reinterpret_cast<uint32_t*>(C) + 3, 1u << (16 + hb));
+        }
     }
 }
 
@@ -4880,6 +4991,7 @@ struct pii_engine {
     uint32_t* lane_split = nullptr;    // k_scan2: per slot split point | A's arena capacity (k_lane_bits2)
     uint32_t* lane_spl = nullptr;      // the same per lane (k_lane_count)
     bool scan2 = false;                // two chains per lane in the SCAN (PII_SCAN2=1: k_scan2; slower)
+    uint32_t halo_items = HALO_ITEMS;  // k_win_halo's item list per workgroup (PII_HALO_ITEMS: tests)
     EvLoc* evloc = nullptr;
     uint64_t ev_cap = 0;
     uint64_t* lane_ev = nullptr;      // exclusive scan of lane_cnt: first dense event index per lane
@@ -5711,9 +5823,13 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
     const WinRing W{e->wr_desc, e->wr_cnt, e->wr_head, e->wr_arena, e->win_n, e->win_slot_bytes, e->n_slots, 0};
     const WinBatch B{text, offs, slot, e->wc, e->wc_first, e->wc_n, n_utt};
     const uint32_t nb = (n_utt + 255) / 256;
-    if (n_utt > 0 && n_chunks > 0)
-        (e->img_eval.global ? k_win_halo<true> : k_win_halo<false>)<<<nb, 256, e->img_eval.lds(), st>>>(
-            e->img_eval.d, e->img_eval.li, W, B, e->wc, e->d_err);
+    if (n_utt > 0 && n_chunks > 0 && R.n_hot > 0) {
+        // (the image in LDS when it fits beside the halo tables, else read in place)
+        const bool hg = e->img_eval.global || ((size_t)e->img_eval.li.total + 15) / 16 * 16 + HALO_LDS > IMG_LDS_MAX;
+        const size_t hl = (hg ? 0 : ((size_t)e->img_eval.li.total + 15) / 16 * 16) + HALO_LDS;
+        (hg ? k_win_halo<true> : k_win_halo<false>)<<<(n_utt + HALO_ROWS - 1) / HALO_ROWS, HALO_ROWS, hl, st>>>(
+            e->img_eval.d, e->img_eval.li, W, B, e->wc, e->halo_items, e->d_err);
+    }
     if (e->timing >= 2) HIPCHK(hipEventRecord(e->tev[3], st));
     if (n_utt > 0) {
         k_win_plan<<<nb, 256, 0, st>>>(W, B, e->wbound, e->wnew, e->d_err);
@@ -6250,7 +6366,11 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             {(const void*)k_select<false, true, true>, &e->img_sel}, {(const void*)k_sel_fix<false, true, true>, &e->img_sel},
             {(const void*)k_pair_eval<false, false, true>, &e->img_eval},
             {(const void*)k_win_eval<false>, &e->img_eval},
-            {(const void*)k_win_select<false>, &e->img_wsel}, {(const void*)k_win_halo<false>, &e->img_eval}};
+            {(const void*)k_win_select<false>, &e->img_wsel}};
+        // k_win_halo<false>: its image plus HALO_LDS of tables (the launch falls back to <true> past the LDS)
+        if (hipFuncSetAttribute((const void*)k_win_halo<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)IMG_LDS_MAX) != hipSuccess)
+            return fail("cannot raise the LDS limit of k_win_halo");
         for (auto& kb : big)
             if (!kb.second->global && kb.second->li.total > 64 * 1024 &&
                 hipFuncSetAttribute(kb.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kb.second->li.total) !=
@@ -6319,6 +6439,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("hipMalloc failed");
     }
     if (const char* v = std::getenv("PII_SCAN2")) e->scan2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PII_HALO_ITEMS")) e->halo_items = (uint32_t)std::max(0, std::min(HALO_ITEMS, std::atoi(v)));
     if (const char* v = std::getenv("PII_TIMING")) e->timing = std::max(0, std::min(2, std::atoi(v)));
     if (max_lds > 64 * 1024 &&
         (hipFuncSetAttribute((const void*)k_scan2<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds) !=

@@ -16,12 +16,26 @@ from conftest import pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["incremental", "full"])
+@pytest.fixture(scope="module", params=["incremental", "full", "incremental_inline_halo"])
 def weng(compiled, request):
+    """incremental_inline_halo: k_win_halo's per-workgroup item list sized 0 (PII_HALO_ITEMS, read at
+    create), so every before-window re-run takes the list-full path in the row's own thread"""
+    import os
     E = pkg("engine")
-    e = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
+    inline = request.param == "incremental_inline_halo"
+    old = os.environ.get("PII_HALO_ITEMS")
+    if inline:
+        os.environ["PII_HALO_ITEMS"] = "0"
+    try:
+        e = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
+    finally:
+        if inline:
+            if old is None:
+                os.environ.pop("PII_HALO_ITEMS", None)
+            else:
+                os.environ["PII_HALO_ITEMS"] = old
     e.window_enable(5, 8192, full=request.param == "full")
-    assert e.window_mode() == request.param
+    assert e.window_mode() == ("full" if request.param == "full" else "incremental")
     yield e
     e.close()
 
