@@ -256,8 +256,16 @@ __global__ __launch_bounds__(256) void k_chunk_index(const uint64_t* __restrict_
             ol[k] = (uint32_t)len;
             kv[k] = (role[u] == PII_ROLE_AGENT && kw_always != KW_NONE) ? kw_always : -1;
             if (wc_n) wc_n[u] = 0;
-            if (len > long_min && cut_row(o[k + 1] - base, o[k + 2] - base, r0, lane_shift, n_chunks, long_min)) {
-                const uint32_t at = atomicAdd(long_count, 1u);
+            const bool cut = len > long_min && cut_row(o[k + 1] - base, o[k + 2] - base, r0, lane_shift, n_chunks, long_min);
+            // one counter atomic per wavefront (a window step cuts ~1k short rows: one atomic per row
+            // serialised on the counter, 7 -> 20 us)
+            const uint64_t bal = __ballot(cut);
+            uint32_t wbase = 0;
+            const int lane = threadIdx.x & 63, lead = bal ? __builtin_ctzll(bal) : 0;
+            if (bal && lane == lead) wbase = atomicAdd(long_count, (uint32_t)__popcll(bal));
+            wbase = __shfl(wbase, lead);
+            if (cut) {
+                const uint32_t at = wbase + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
                 if (at < long_cap) {
                     long_rows[at] = u;
                 } else {
@@ -793,6 +801,9 @@ __device__ __forceinline__ void emit_range(const Lane& L, uint32_t& e_lo, uint32
 // a WIDE group's table (one workgroup per CU: 16 waves instead of 12).  (256-thread workgroups for the
 // window re-scan's small steps, to reach every CU instead of 123: 67 -> 73 us, not kept)
 constexpr int SCAN_BLOCK_WIDE = 1024;
+#ifndef SCAN_ABLATE
+#define SCAN_ABLATE 0               // measurement builds only: 1 = k_scan returns after its table load
+#endif
 template <bool HK, int NT = SCAN_BLOCK>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_BLOCK ? SCAN1_WAVES : 4, NT == SCAN_BLOCK ? SCAN1_WAVES : 4))) void k_scan(const RulesDev R, const Geo g, const uint8_t* __restrict__ text,
                                                      const uint64_t* __restrict__ words,
@@ -820,6 +831,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
     __syncthreads();
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
     if (t >= g.n_chunks) return;
+#if SCAN_ABLATE == 1
+    if (g.n_chunks != 0xffffffffu) return;      // (measurement: the table load only)
+#endif
     const uint32_t c = lane_perm[t];
     const Lane L = g_lane(g, c);
     // positions relative to the batch base fit 32 bits (PII_MAX_BATCH_BYTES); 32-bit arithmetic keeps
@@ -1268,7 +1282,11 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev* __restrict__ R
     uint32_t& s_full = s_prev[FIX_Q + 2];
     const uint32_t nrows = *long_count;
     if (blockIdx.x >= nrows || (*err & (ERR_ARGS | ERR_STITCH))) return;     // (STITCH: the row list overflowed)
-    {
+    // the scan tables are staged in LDS only once a boundary needs a re-scan (the halo guesses are
+    // almost always right: checking them needs no table, and a window step's ~1k short cut rows paid
+    // a 62 KB table load per workgroup for nothing)
+    bool staged = false;
+    auto stage = [&]() {
         const int nd_words = R.SD * R.CDs / 2, nk_words = R.SK * R.CKs / 2;
         const uint32_t* g_td = reinterpret_cast<const uint32_t*>(R.td);
         const uint32_t* g_tk = reinterpret_cast<const uint32_t*>(R.tk);
@@ -1277,8 +1295,9 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev* __restrict__ R
         for (int i = threadIdx.x; i < 256; i += blockDim.x) smem32[i] = R.cmap4[i];
         for (int i = threadIdx.x; i < nd_words; i += blockDim.x) d_td[i] = g_td[i];
         for (int i = threadIdx.x; i < nk_words; i += blockDim.x) d_tk[i] = g_tk[i];
-    }
-    __syncthreads();
+        __syncthreads();
+        staged = true;
+    };
     for (uint32_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
         uint32_t ca, kb;
         int64_t s_r, e_r;
@@ -1330,6 +1349,7 @@ __global__ __launch_bounds__(256) void k_scan_fix(const RulesDev* __restrict__ R
             __syncthreads();
             const uint32_t n = min(s_n, (uint32_t)FIX_Q);
             if (n == 0 && !s_full) break;
+            if (!staged) stage();                       // (n and s_full are block-uniform here)
             for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
                 rescan_lane(R, g, text, s_q[k], s_e[k], ev, lane_cnt, lane_st);
             __syncthreads();
@@ -4096,7 +4116,20 @@ __global__ __launch_bounds__(PAIR_BLOCK) void k_win_eval(const uint4* __restrict
 // per scan lane: finditer skipping per pattern over the lane's matched pairs (variant independent),
 // then the validator-passing survivors become the rows' resident candidates (wc, in pair-queue slots
 // of the lane: a lane never has more candidates than pairs)
-__global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint64_t* __restrict__ lane_pair,
+// leading pairs of lane c that belong to row r (a row cut at the lane's lo): the lane's pairs are in
+// position order, so a binary search over their rows
+__device__ __forceinline__ uint32_t lead_pairs(const PairRes* __restrict__ pres, const EvLoc* __restrict__ evloc,
+                                               uint64_t base, uint32_t np, uint32_t r) {
+    uint32_t lo = 0, hi = np;                      // first pair whose row is not r
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (evloc[pres[base + mid].ev].u == r) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_win_cands(const Geo g, const uint64_t* __restrict__ lane_pair,
                                                    const uint32_t* __restrict__ lane_np,
                                                    const EvLoc* __restrict__ evloc, const PairRes* __restrict__ pres,
                                                    const int32_t* __restrict__ pend, const uint32_t* __restrict__ phot,
@@ -4104,11 +4137,19 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
                                                    uint32_t* __restrict__ wc_first, uint32_t* __restrict__ wc_n,
                                                    const uint32_t* __restrict__ err) {
     if (*err & ERR_ABORT) return;
+    const uint32_t n_chunks = g.n_chunks;
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
-    const uint32_t np = lane_np[c];
-    const uint64_t base = lane_pair[c];
-    if (np == 0 || base + np > pair_cap) return;
+    const Lane L = g_lane(g, c);
+    const uint32_t np0 = lane_np[c];
+    if (lane_pair[c] + np0 > pair_cap) return;
+    // A row cut into several lanes (rows longer than long_min) is walked whole by the thread of the
+    // lane holding its start: it continues into the next lanes' leading pairs, which their own
+    // threads skip.  Its candidates and spill list run on past the lane's slots into the next lanes'
+    // (never further than the pairs it has walked), so a lane's own rows start behind the skipped ones.
+    const uint32_t i0 = L.clo ? lead_pairs(pres, evloc, lane_pair[c], np0, L.u0) : 0u;
+    const uint64_t base = lane_pair[c] + i0;       // this thread's wc / spill slots
+    const uint32_t np = np0 - i0;
     uint32_t u = 0xffffffffu, k = 0, uf = 0;
     int lp[LIVE], le[LIVE];
     // more than LIVE patterns live in one row: their (pattern, end) list in the lane's pair-queue slots
@@ -4121,8 +4162,8 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         lp[q] = -1;
         le[q] = -1;
     }
-    auto cand = [&](uint32_t i, int e) {
-        const PairRes P = pres[base + i];
+    auto cand = [&](uint64_t pi, int e) {            // pi: pair index
+        const PairRes P = pres[pi];
         const EvLoc Lc = evloc[P.ev];
         const int s = (int)(Lc.s - Lc.ustart);
         if (Lc.u != u) {
@@ -4188,31 +4229,47 @@ __global__ __launch_bounds__(256) void k_win_cands(uint32_t n_chunks, const uint
         C.p = (uint16_t)p;
         C.need = 0;
         C.pad = 0;
-        C.hot = (uint16_t)phot[base + i];
+        C.hot = (uint16_t)phot[pi];
         C.hotx = C.hot;
         wc[base + k++] = C;
     };
-    // the lane's pend[] run in prefetched 16-entry groups, matched pairs only (as in k_select)
-    const uint32_t off0 = (uint32_t)(base & 3u);
-    const int4* pa = reinterpret_cast<const int4*>(pend + (base - off0));
-    const uint32_t ng = (off0 + np + 15u) >> 4;
-    int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
-    for (uint32_t g = 0; g < ng; ++g) {
-        const int4 c0 = q0, c1 = q1, c2 = q2, c3 = q3;
-        if (g + 1 < ng) {
-            const int4* pn = pa + 4 * (g + 1);
-            q0 = pn[0];
-            q1 = pn[1];
-            q2 = pn[2];
-            q3 = pn[3];
+    // the matched pairs of the pend[] run [pb, pb + n) in prefetched 16-entry groups (as in k_select)
+    auto walk = [&](uint64_t pb, uint32_t n) {
+        if (n == 0) return;
+        const uint32_t off0 = (uint32_t)(pb & 3u);
+        const int4* pa = reinterpret_cast<const int4*>(pend + (pb - off0));
+        const uint32_t ng = (off0 + n + 15u) >> 4;
+        int4 q0 = pa[0], q1 = pa[1], q2 = pa[2], q3 = pa[3];
+        for (uint32_t gi = 0; gi < ng; ++gi) {
+            const int4 c0 = q0, c1 = q1, c2 = q2, c3 = q3;
+            if (gi + 1 < ng) {
+                const int4* pn = pa + 4 * (gi + 1);
+                q0 = pn[0];
+                q1 = pn[1];
+                q2 = pn[2];
+                q3 = pn[3];
+            }
+            const uint32_t g0 = 16u * gi;
+            uint32_t m = matched_mask16(c0, c1, c2, c3, g0, off0, n);
+            while (m) {
+                const uint32_t j = (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                const uint64_t pi = pb + (g0 + j - off0);
+                cand(pi, pend[pi]);
+            }
         }
-        const uint32_t g0 = 16u * g;
-        uint32_t m = matched_mask16(c0, c1, c2, c3, g0, off0, np);
-        while (m) {
-            const uint32_t j = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            const uint32_t i = g0 + j - off0;
-            cand(i, pend[base + i]);
+    };
+    walk(base, np);
+    // the lane's last row continues into the next lanes: their leading pairs
+    if (L.chi) {
+        const uint32_t r = L.u1 - 1;
+        for (uint32_t c2 = c + 1; c2 < n_chunks; ++c2) {
+            const uint32_t n2 = lane_np[c2];
+            const uint64_t b2 = lane_pair[c2];
+            if (b2 + n2 > pair_cap) break;
+            walk(b2, lead_pairs(pres, evloc, b2, n2, r));
+            const Lane L2 = g_lane(g, c2);
+            if (!(L2.chi && L2.u1 - 1 == r)) break;
         }
     }
     if (u != 0xffffffffu && k > uf) {
@@ -4992,6 +5049,7 @@ struct pii_engine {
     uint32_t* lane_spl = nullptr;      // the same per lane (k_lane_count)
     bool scan2 = false;                // two chains per lane in the SCAN (PII_SCAN2=1: k_scan2; slower)
     uint32_t halo_items = HALO_ITEMS;  // k_win_halo's item list per workgroup (PII_HALO_ITEMS: tests)
+    uint32_t win_long = 0;             // incremental re-scan: rows longer than this many lanes are cut (PII_WIN_LONG; 0: never)
     EvLoc* evloc = nullptr;
     uint64_t ev_cap = 0;
     uint64_t* lane_ev = nullptr;      // exclusive scan of lane_cnt: first dense event index per lane
@@ -5795,7 +5853,11 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
                                span_cap, win_ctx, st);
     e->lane_shift = pick_lane_shift(e, total_bytes);
     e->r0 = (uint32_t)(((uintptr_t)text + base) & 63);
-    e->long_min = NO_CUTS;                      // the window kernels keep rows whole
+    // rows whole by default; PII_WIN_LONG = n cuts rows longer than n lanes like the main path's long
+    // rows (k_win_cands then walks a cut row whole).  A step's scan takes as long as its longest lane
+    // (a whole 750-byte row of 128-byte lanes), and cutting at 2 lanes takes k_scan 67 -> 53 us, but
+    // the stitching, the long-row list and the cut-row candidate walk cost more
+    e->long_min = e->win_long ? e->win_long << e->lane_shift : NO_CUTS;
     const uint32_t n_chunks = lane_count(e, total_bytes);
     e->last_lanes = n_chunks;
     int rc = ensure_scratch(e, n_utt, total_bytes, n_chunks);
@@ -5815,7 +5877,7 @@ int run_window(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint32_
         (e->img_eval.global ? k_win_eval<true> : k_win_eval<false>)<<<e->n_seg, PAIR_BLOCK, e->img_eval.lds(), st>>>(
             e->img_eval.d, e->img_eval.li, text, offs, pcount, e->pair_cap, e->matched, e->mcount, e->n_seg,
             e->evloc, e->pend, e->pres, e->phot);
-        k_win_cands<<<(n_chunks + 255) / 256, 256, 0, st>>>(n_chunks, e->lane_pair, e->lane_np, e->evloc, e->pres,
+        k_win_cands<<<(n_chunks + 255) / 256, 256, 0, st>>>(make_geo(e, offs, n_utt, n_chunks, base), e->lane_pair, e->lane_np, e->evloc, e->pres,
                                                             e->pend, e->phot, e->pair_cap, e->spill, e->wc, e->wc_first,
                                                             e->wc_n, e->d_err);
         HIPCHK(hipGetLastError());
@@ -6439,6 +6501,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("hipMalloc failed");
     }
     if (const char* v = std::getenv("PII_SCAN2")) e->scan2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PII_WIN_LONG")) e->win_long = (uint32_t)std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("PII_HALO_ITEMS")) e->halo_items = (uint32_t)std::max(0, std::min(HALO_ITEMS, std::atoi(v)));
     if (const char* v = std::getenv("PII_TIMING")) e->timing = std::max(0, std::min(2, std::atoi(v)));
     if (max_lds > 64 * 1024 &&

@@ -16,24 +16,30 @@ from conftest import pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["incremental", "full", "incremental_inline_halo"])
+# engine environment per variant (read at create): incremental_inline_halo sizes k_win_halo's
+# per-workgroup item list 0, so every before-window re-run takes the list-full path in the row's own
+# thread; incremental_cut1 / _cut2 cut every row longer than one / two scan lanes (PII_WIN_LONG; by
+# default rows stay whole): k_win_cands' cross-lane rows, the halo states and their stitching
+_WENV = {"incremental_inline_halo": {"PII_HALO_ITEMS": "0"}, "incremental_cut1": {"PII_WIN_LONG": "1"},
+         "incremental_cut2": {"PII_WIN_LONG": "2"}}
+
+
+@pytest.fixture(scope="module", params=["incremental", "full", "incremental_inline_halo", "incremental_cut1",
+                                        "incremental_cut2"])
 def weng(compiled, request):
-    """incremental_inline_halo: k_win_halo's per-workgroup item list sized 0 (PII_HALO_ITEMS, read at
-    create), so every before-window re-run takes the list-full path in the row's own thread"""
     import os
     E = pkg("engine")
-    inline = request.param == "incremental_inline_halo"
-    old = os.environ.get("PII_HALO_ITEMS")
-    if inline:
-        os.environ["PII_HALO_ITEMS"] = "0"
+    env = _WENV.get(request.param, {})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         e = E.Engine(compiled.blob, device=0, n_conv_slots=4096)
     finally:
-        if inline:
-            if old is None:
-                os.environ.pop("PII_HALO_ITEMS", None)
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["PII_HALO_ITEMS"] = old
+                os.environ[k] = v
     e.window_enable(5, 8192, full=request.param == "full")
     assert e.window_mode() == ("full" if request.param == "full" else "incremental")
     yield e
