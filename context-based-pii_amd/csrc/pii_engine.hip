@@ -809,7 +809,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
                                                      const uint64_t* __restrict__ words,
                                                      const uint32_t* __restrict__ lane_perm, Event* __restrict__ ev,
                                                      uint32_t* __restrict__ lane_cnt, uint32_t* __restrict__ lane_st,
-                                                     const uint32_t* __restrict__ err) {
+                                                     const uint32_t* __restrict__ err, uint32_t ilv) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
     if (*err & ERR_ARGS) return;              // the declared batch size was wrong: nothing is sized for it
     // LDS: class map at 0 (256 x class words: D base + 2 classD | (K base + 2 classK) << 16), D table,
@@ -829,7 +829,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == SCAN_B
         for (int i = threadIdx.x; i < 128; i += blockDim.x) d_sp[i] = scan_spread(2 * i) | scan_spread(2 * i + 1) << 16;
     }
     __syncthreads();
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;      // slot (lanes longest first)
+    // slot (lanes longest first).  ilv (a grid of at most one workgroup per CU): the wavefronts are
+    // dealt round-robin over the workgroups, so the longest lanes run one wavefront per CU instead of
+    // sharing the first CU's LDS
+    const uint32_t t = ilv ? ((threadIdx.x >> 6) * gridDim.x + blockIdx.x) * 64u + (threadIdx.x & 63u)
+                           : blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= g.n_chunks) return;
 #if SCAN_ABLATE == 1
     if (g.n_chunks != 0xffffffffu) return;      // (measurement: the table load only)
@@ -5049,6 +5053,7 @@ struct pii_engine {
     uint32_t* lane_spl = nullptr;      // the same per lane (k_lane_count)
     bool scan2 = false;                // two chains per lane in the SCAN (PII_SCAN2=1: k_scan2; slower)
     uint32_t halo_items = HALO_ITEMS;  // k_win_halo's item list per workgroup (PII_HALO_ITEMS: tests)
+    bool scan_ilv = true;              // k_scan grids of <= n_cu workgroups deal wavefronts round-robin (PII_SCAN_ILV)
     uint32_t win_long = 0;             // incremental re-scan: rows longer than this many lanes are cut (PII_WIN_LONG; 0: never)
     EvLoc* evloc = nullptr;
     uint64_t ev_cap = 0;
@@ -5494,9 +5499,10 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                         Rq, g, text, reinterpret_cast<const uint32_t*>(e->bnd), e->lane_split, e->lane_perm, evq,
                         cq, stq, e->d_err);
                 } else {
+                    const uint32_t nb = (n_chunks + nt - 1) / nt;
                     (q == 0 ? k_scan<true> : one_wg ? k_scan<false, SCAN_BLOCK_WIDE> : k_scan<false>)<<<
-                        (n_chunks + nt - 1) / nt, nt, e->sg_lds[q], sq>>>(
-                        Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err);
+                        nb, nt, e->sg_lds[q], sq>>>(Rq, g, text, e->bnd, e->lane_perm, evq, cq, stq, e->d_err,
+                                                    e->scan_ilv && nb <= e->n_cu ? nb : 0u);
                 }
             }
             for (uint32_t i = 0; i + 1 < ns_scan; ++i) {
@@ -6501,6 +6507,7 @@ int pii_engine_create(const void* blob, size_t n, int device, uint32_t n_conv_sl
             return fail("hipMalloc failed");
     }
     if (const char* v = std::getenv("PII_SCAN2")) e->scan2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PII_SCAN_ILV")) e->scan_ilv = std::atoi(v) != 0;
     if (const char* v = std::getenv("PII_WIN_LONG")) e->win_long = (uint32_t)std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("PII_HALO_ITEMS")) e->halo_items = (uint32_t)std::max(0, std::min(HALO_ITEMS, std::atoi(v)));
     if (const char* v = std::getenv("PII_TIMING")) e->timing = std::max(0, std::min(2, std::atoi(v)));
