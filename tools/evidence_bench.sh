@@ -17,4 +17,6 @@ run scan 600 && run window 300 --workload window --steps 20 --warmup 5 --no-cpu-
 run window_config5 600 --workload window --window-rules config5 --conversations 50000 --steps 10 --warmup 5 --no-cpu-baseline && \
 run config5 600 --workload config5 --no-cpu-baseline && run long 300 --workload long --no-cpu-baseline && \
 run stream 600 --workload stream --no-cpu-baseline && run ner 300 --workload ner --no-cpu-baseline && \
-run ner-redact 300 --workload ner-redact --no-cpu-baseline && echo EVIDENCE_B_OK
+run ner-redact 300 --workload ner-redact --no-cpu-baseline && \
+run service8 300 --workload service --clients 8 --no-cpu-baseline && \
+run service64 300 --workload service --clients 64 --no-cpu-baseline && echo EVIDENCE_B_OK
