@@ -4853,6 +4853,18 @@ __global__ void k_ctx_totals(const uint32_t* __restrict__ err, uint64_t* __restr
     totals[3] = totals[4] = totals[5] = 0;
 }
 
+// a call's first kernel: its counter block (err, long_count, ncommit, pair_count) from zero or from a
+// first pass's block, the lane-sort buckets, and a histogram reset deferred to here (three memset /
+// copy commands were ~15 us of gaps per call)
+__global__ __launch_bounds__(256) void k_begin(uint32_t* __restrict__ d_err, const uint32_t* __restrict__ err_init,
+                                               uint32_t* __restrict__ lane_bkt, uint32_t nbkt,
+                                               unsigned long long* __restrict__ hist, uint32_t nhist) {
+    const uint32_t t = threadIdx.x;
+    if (t < 6) d_err[t] = err_init ? err_init[t] : 0u;
+    for (uint32_t i = t; i < nbkt; i += blockDim.x) lane_bkt[i] = 0;
+    for (uint32_t i = t; i < nhist; i += blockDim.x) hist[i] = 0;
+}
+
 __global__ void k_noop() {}
 
 // ------------------------------------------------------------------------------- LDS images
@@ -5101,7 +5113,7 @@ struct pii_engine {
     uint64_t* d_totals = nullptr;
     uint64_t* h_totals = nullptr;    // pinned copy of d_totals (+ the histogram behind it)
     bool h_hist_valid = false;       // h_totals' histogram is the device's as of the last call (no reset since)
-    bool reset_pending = false;      // a histogram reset was enqueued on `stream` and not yet ordered
+    bool hist_zero_pending = false;  // pii_histogram_reset since the last call: its k_begin zeroes the histogram
     // host-API staging
     uint64_t cap_h_bytes = 0, cap_h_out = 0;
     uint32_t cap_h_utt = 0, cap_h_spans = 0;
@@ -5427,14 +5439,13 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
                  int16_t* ctx, int16_t* win_ctx, const unsigned long long* pcount, hipStream_t st,
                  const uint32_t* err_init = nullptr, bool ctx_kernels = true, bool pair_first = true) {
     const RulesDev& R = e->R;
-    if (e->reset_pending && st != e->stream) HIPCHK(hipStreamSynchronize(e->stream));   // order the reset
-    e->reset_pending = false;
     e->epoch += 1;
     const Geo g = make_geo(e, offs, n_utt, n_chunks, base);
-    if (err_init)              // a second pass over the call: start from the first pass's counter block
-        HIPCHK(hipMemcpyAsync(e->d_err, err_init, 24, hipMemcpyDeviceToDevice, st));
-    else
-        HIPCHK(hipMemsetAsync(e->d_err, 0, 24, st));   // err, long_count, ncommit, pair_count
+    // counter block (a second pass over the call starts from the first pass's), lane buckets, and the
+    // histogram if pii_histogram_reset was called since the last call
+    k_begin<<<1, 256, 0, st>>>(e->d_err, err_init, e->lane_bkt, n_chunks > 0 ? 2u * LANE_NB : 0u, e->hist,
+                               e->hist_zero_pending ? (uint32_t)std::max(e->R.T, 256) : 0u);
+    e->hist_zero_pending = false;
     if (e->timing >= 1) HIPCHK(hipEventRecord(e->tev[0], st));
     if (n_utt > 0) {
         k_chunk_index<<<(n_utt / CI_ROWS + 1 + 255) / 256, 256, 0, st>>>(offs, role, n_utt, n_chunks, e->lane_shift, e->r0,
@@ -5450,7 +5461,6 @@ int launch_front(pii_engine* e, const uint8_t* text, const uint64_t* offs, uint3
             // step: 128-512-byte lanes of one or two rows) have no utterance start to split at
             const bool split = e->scan2 && e->lane_shift == (uint32_t)__builtin_ctz(BYTES_PER_LANE) &&
                                e->long_min != NO_CUTS && e->n_sg == 1;
-            HIPCHK(hipMemsetAsync(e->lane_bkt, 0, 2 * LANE_NB * sizeof(uint32_t), st));
             const uint32_t nsb = (n_chunks + LANE_SORT_CHUNK - 1) / LANE_SORT_CHUNK;
             Geo g0 = g;
             g0.lanes = nullptr;
@@ -7149,6 +7159,10 @@ int pii_histogram(pii_engine* e, uint64_t* counts, uint32_t n) {
     if (!e || !counts) return PII_E_ARG;
     HIPCHK(hipSetDevice(e->device));
     const uint32_t T = (uint32_t)e->R.T;
+    if (e->hist_zero_pending) {    // reset since the last call: the next call zeroes the device copy
+        for (uint32_t i = 0; i < n; ++i) counts[i] = 0;
+        return PII_OK;
+    }
     if (e->h_hist_valid) {         // the last call copied it with its totals: no extra round trip
         HIPCHK(hipEventSynchronize(e->tev[6]));
         const uint64_t* h = e->h_totals + 8;
@@ -7162,16 +7176,13 @@ int pii_histogram(pii_engine* e, uint64_t* counts, uint32_t n) {
     return PII_OK;
 }
 
-// stream-ordered: the next call on the engine's stream starts from zero (no host wait here). The
-// memset first waits for the last call's end event, which that call recorded on ITS stream (a
-// caller stream for the _ex entry points), so the reset never races that call's k_hist_reduce.
+// deferred: the next call's first kernel (k_begin) zeroes the histogram on that call's stream, after
+// the previous call (calls are sequential: each is followed by pii_sync); until then pii_histogram
+// reports zeros.  No device command and no host wait here.
 int pii_histogram_reset(pii_engine* e) {
     if (!e) return PII_E_ARG;
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamWaitEvent(e->stream, e->tev[6], 0));
-    HIPCHK(hipMemsetAsync(e->hist, 0, std::max(e->R.T, 256) * 8, e->stream));
     e->h_hist_valid = false;
-    e->reset_pending = true;
+    e->hist_zero_pending = true;
     return PII_OK;
 }
 

@@ -184,8 +184,9 @@ int pii_context_update(struct pii_engine* e, const uint8_t* bytes, const uint64_
 
 /* per-info-type counts of kept findings since the last reset (counts[n_types]); the multi-GPU
  * driver all-reduces these over RCCL.  Each call copies the counts to pinned host memory with its
- * totals, so reading them after pii_sync costs no further device round trip.  The reset is
- * stream-ordered (no host wait): the next call starts from zero, on any stream. */
+ * totals, so reading them after pii_sync costs no further device round trip.  The reset issues no
+ * device command: the next call's first kernel zeroes the counts (on that call's stream), and until
+ * that call pii_histogram reports zeros. */
 int pii_histogram(struct pii_engine* e, uint64_t* counts, uint32_t n);
 int pii_histogram_reset(struct pii_engine* e);
 

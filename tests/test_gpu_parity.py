@@ -180,13 +180,23 @@ def test_context_ttl_and_persistence(eng, oracle_cfg):
 
 
 def test_histogram_matches_spans(eng, oracle_cfg):
+    """counts accumulate over calls until pii_histogram_reset; the reset is deferred to the next call's
+    first kernel, and the counts read as zero until then"""
     synth = pkg("synth")
     bank = synth.build_bank(100, 400, seed=3)
     eng.histogram_reset()
+    assert not eng.histogram().any()
     res = eng.scan_redact(bank.texts, list(range(40000, 40000 + len(bank.texts))), list(bank.roles))
     h = eng.histogram()
     want = np.bincount(res.spans["info_type"].astype(np.int64), minlength=len(h))
-    assert (h == want).all()
+    assert want.any() and (h == want).all()
+    res2 = eng.scan_redact(bank.texts[:50], list(range(41000, 41050)), list(bank.roles[:50]))
+    want2 = np.bincount(res2.spans["info_type"].astype(np.int64), minlength=len(h))
+    assert (eng.histogram() == want + want2).all()
+    eng.histogram_reset()
+    assert not eng.histogram().any()
+    res3 = eng.scan_redact(bank.texts[:50], list(range(42000, 42050)), list(bank.roles[:50]))
+    assert (eng.histogram() == np.bincount(res3.spans["info_type"].astype(np.int64), minlength=len(h))).all()
 
 
 def test_device_api_large_batch_properties(eng, oracle_cfg):
